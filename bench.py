@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""STOMP iterations/sec on MI355X (BASELINE.json metric), one JSON line on rank 0.
+
+Workload (BASELINE.json configs[1], "cfg2"): 7-DOF PR2-like arm, 100 waypoints
+(N = 99 free), K = 512 noisy rollouts per GPU, no reuse, 256^3 fp32 distance
+field of the shelf + pole scene, built on the device.  A step is one
+PolicyImprovementLoop::runSingleIteration equivalent (noise, projection, control
+costs, K rollout executions, probability weighting, update, noiseless rollout),
+enqueued by stomp_engine_run with inputs already resident in HBM.  With --gpus N
+the K dimension is sharded (K = 512 N, weak scaling) and the per-iteration
+reductions run over RCCL inside the engine.
+
+Also reported:
+  roofline      dominant kernel (rollout_cost): algorithmic bytes per launch
+                K_gen * N * (4 S + 8 J + 8) over its HIP-event duration in the timed region
+  cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread)
+                timed on this host on a bounded sample of the same workload
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "STOMP iterations/sec (7-DOF, 100 wp, K=512, 256³ SDF) at 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rollouts-per-gpu", type=int, default=512)
+    ap.add_argument("--waypoints", type=int, default=100)
+    ap.add_argument("--dof", type=int, default=7)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--no-timing", action="store_true", help="no HIP events in the timed region")
+    return ap.parse_args()
+
+
+def latest_traffic():
+    """HBM bytes per rollout_cost launch from the newest committed rocprofv3 PMC summary, if any."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*rollout_cost_traffic*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(problem, budget_s: float):
+    from oracle import pyoracle as po
+    o = po.Oracle(problem, dense=True, threads=1)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        o.iterate(n + 1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 200:
+            break
+    return {"value": n / el, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} iterations of the same workload (K={problem.params.num_rollouts}, N={problem.N}, "
+                      f"J={problem.J}, {problem.grid.n}^3 SDF) on the CPU oracle in reference structure "
+                      f"(dense N x N products, sequential Task::execute), 1 thread, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # CPU rendezvous only: the data path is RCCL inside the engine
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from stomp_motion_planner_icra2011_amd import engine as eng
+    from stomp_motion_planner_icra2011_amd import problem as pb
+
+    K = args.rollouts_per_gpu * world
+    p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
+                        num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + args.steps + 1)
+    sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
+    eng.sdf_build_device(p, sdf.ptr)
+    comm_id = None
+    if world > 1:
+        obj = [eng.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    e = eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr, rank=rank, world_size=world, comm_id=comm_id)
+
+    # warmup
+    e.run(1, args.warmup)
+    e.synchronize()
+    if not args.no_timing:
+        e.set_timing(True)
+    if dist:
+        dist.barrier()
+    e.synchronize()
+    t0 = time.perf_counter()
+    e.run(args.warmup + 1, args.steps)
+    e.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = args.steps / elapsed
+
+    timing = {}
+    if not args.no_timing:
+        for name in ("noise", "rollout_cost", "weights", "update", "noiseless", "all"):
+            tot, n = e.timing(name)
+            timing[name] = {"total_ms": tot, "launches": n, "avg_us": 1000.0 * tot / max(n, 1)}
+        e.set_timing(False)
+
+    S = len(p.spheres)
+    K_loc = e.K_loc
+    bytes_per_launch = K_loc * p.N * (4 * S + 8 * p.J + 8)
+    roofline = None
+    if timing.get("rollout_cost", {}).get("launches"):
+        avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
+        achieved = bytes_per_launch / avg_s / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": latest_traffic(),
+                    "kernel": "k_rollout_cost", "bytes_per_launch": bytes_per_launch,
+                    "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        pc = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
+                             num_reused_rollouts=0)
+        cpu = cpu_baseline(pc, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (PR2-like arm, shelf+pole scene, device-built SDF; Philox noise)",
+            "config": {"workload": f"cfg2: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={args.rollouts_per_gpu}/GPU "
+                                   f"(K={K} total), K_r=0, {args.grid}^3 SDF, S={S} spheres",
+                       "rollouts_per_gpu": args.rollouts_per_gpu, "global_rollouts": K,
+                       "parallelism": f"rollout shard x{world}" + (" (RCCL)" if world > 1 else ""),
+                       "rollouts_per_s": round(value * K, 1)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_timing_us": {k: round(v["avg_us"], 3) for k, v in timing.items()},
+        }
+        print(json.dumps(out))
+    e.close()
+    sdf.free()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

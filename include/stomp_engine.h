@@ -1,0 +1,206 @@
+/*
+ * stomp_engine.h -- C ABI of the MI355X STOMP noisy-rollout cost engine.
+ *
+ * Drop-in boundary for the hot path of kalakris/stomp_motion_planner_icra2011
+ * (paths relative to /root/reference/stomp_motion_planner/):
+ *
+ *   stomp_engine_create      replaces StompOptimizer::StompOptimizer + initialize()
+ *                            (stomp_optimizer.cpp:50-202) together with
+ *                            PolicyImprovementLoop::initialize (policy_improvement_loop.cpp:88-110),
+ *                            PolicyImprovement::initialize (policy_improvement.cpp:64-94) and
+ *                            CovariantTrajectoryPolicy::initialize/setToMinControlCost
+ *                            (covariant_trajectory_policy.cpp:70-148)
+ *   stomp_engine_iterate     replaces PolicyImprovementLoop::runSingleIteration
+ *                            (policy_improvement_loop.cpp:143-202)
+ *   stomp_engine_run         the same iteration, enqueued `count` times with no host sync
+ *   stomp_engine_eval        replaces StompOptimizer::execute (stomp_optimizer.cpp:1063-1165),
+ *                            batched over rollouts (Task::execute, task.h:70)
+ *   stomp_engine_optimize    replaces StompOptimizer::optimize (stomp_optimizer.cpp:249-401)
+ *   stomp_engine_get_theta / set_theta
+ *                            replace CovariantTrajectoryPolicy::getParameters/setParameters
+ *                            (covariant_trajectory_policy.h:200-227)
+ *   stomp_sdf_build          builds the distance field that
+ *                            StompCollisionSpace::setStartState + PropagationDistanceField
+ *                            produce (stomp_collision_space.cpp:154-197), for box and
+ *                            z-cylinder obstacles, directly in device memory
+ *
+ * Conventions: plain pointers and sizes only; host buffers are caller-owned and
+ * read/written during the call; device buffers are engine-owned.  Trajectories
+ * and parameters are row-major [joint][time step] doubles (J x N).  Every call
+ * returns 0 on success (the reference's `true`) or a negative STOMP_E_* code;
+ * stomp_engine_last_error() / stomp_last_error() give the message.  Calls on one
+ * engine must be serialised by the caller (the reference is single-threaded,
+ * stomp_planner_node.cpp:547); distinct engines may run concurrently.
+ */
+#ifndef STOMP_ENGINE_H
+#define STOMP_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STOMP_ENGINE_ABI_VERSION 1
+
+#define STOMP_OK 0
+#define STOMP_E_INVALID (-1)   /* bad sizes / arguments */
+#define STOMP_E_DEVICE (-2)    /* HIP runtime failure */
+#define STOMP_E_UNSUPPORTED (-3)
+#define STOMP_E_COMM (-4)      /* RCCL failure */
+
+/* One kinematic-tree segment, DFS order (parent < own index).  Frame of the
+ * segment tip: frame[s] = frame[parent] * Frame(rot, trans) * Frame(Rot2(axis, q), 0)
+ * with q = joint vector[q_index] (q_index = -1: fixed segment).  Replaces the KDL
+ * tree of stomp_robot_model.cpp:81-86 as consumed by
+ * treefksolverjointposaxis_partial.cpp:108-178. */
+typedef struct stomp_segment {
+    int32_t parent;
+    int32_t q_index;
+    double rot[9];
+    double trans[3];
+    double axis[3];
+} stomp_segment;
+
+/* StompCollisionPoint (stomp_collision_point.h:76-82): sphere in a segment frame */
+typedef struct stomp_sphere {
+    int32_t segment;
+    double radius;
+    double clearance;
+    double pos[3];
+} stomp_sphere;
+
+/* StompJoint limits and joint_costs/<name> (stomp_robot_model.h, stomp_optimizer.cpp:107-109) */
+typedef struct stomp_joint {
+    int32_t has_limits;
+    double min;
+    double max;
+    double joint_cost;
+} stomp_joint;
+
+/* Distance field: value(x,y,z) = data[(x*ny + y)*nz + z], metres, fp32.  A
+ * position maps to the cell round((p - origin)/resolution); cells with any index
+ * < 1 or >= n-1 read 0 (distance_field::getDistanceGradient semantics). */
+typedef struct stomp_grid {
+    int32_t nx, ny, nz;
+    double origin[3];
+    double resolution;
+    const float* data;          /* host pointer, or device pointer if data_on_device */
+    int32_t data_on_device;     /* 1: engine uses the buffer in place (caller keeps it alive) */
+} stomp_grid;
+
+typedef struct stomp_engine_desc {
+    int32_t abi_version;        /* STOMP_ENGINE_ABI_VERSION */
+    int32_t num_joints;         /* J (planning group joints) */
+    int32_t num_time_steps;     /* N free waypoints (params.yaml num_time_steps) */
+    int32_t num_rollouts;       /* K (params.yaml num_rollouts), whole job */
+    int32_t num_reused_rollouts;/* K_r (params.yaml num_reused_rollouts) */
+    int32_t num_segments;
+    const stomp_segment* segments;
+    int32_t num_spheres;
+    const stomp_sphere* spheres;
+    const stomp_joint* joints;  /* J */
+    stomp_grid grid;
+    double discretization;      /* trajectory_discretization */
+    double smoothness_costs[3]; /* smoothness_cost_{velocity,acceleration,jerk} */
+    double ridge_factor;
+    double smoothness_cost_weight;
+    double obstacle_cost_weight;
+    double constraint_cost_weight;
+    double torque_cost_weight;  /* > 1e-9 -> STOMP_E_UNSUPPORTED (torque term not built yet) */
+    const double* noise_stddev; /* J */
+    const double* noise_decay;  /* J */
+    int32_t use_cumulative_costs;
+    const double* start;        /* J */
+    const double* goal;         /* J */
+    uint64_t seed;              /* Philox key of the noise stream */
+    int32_t max_iterations;
+    int32_t max_iterations_after_collision_free;
+    int32_t device;             /* HIP device ordinal */
+    void* stream;               /* hipStream_t to launch on; NULL -> engine-owned stream */
+    int32_t rank;               /* rollout shard of this process (0 if world_size == 1) */
+    int32_t world_size;         /* processes sharing the K rollouts (1 = no collectives) */
+    const void* comm_id;        /* 128-byte RCCL unique id from stomp_comm_unique_id (rank 0) */
+} stomp_engine_desc;
+
+typedef struct stomp_engine stomp_engine;
+
+typedef struct stomp_iter_out {
+    double cost;                /* last_trajectory_cost_ of the noiseless rollout */
+    int32_t collision_free;     /* last_trajectory_collision_free_ */
+} stomp_iter_out;
+
+/* STOMPStatistics (msg/STOMPStatistics.msg) without the ROS header / torques */
+typedef struct stomp_stats {
+    int32_t iterations;
+    int32_t success;
+    int32_t success_iteration;
+    int32_t collision_success_iteration;
+    int32_t last_improvement_iteration;
+    double best_cost;
+} stomp_stats;
+
+int stomp_engine_create(const stomp_engine_desc* desc, stomp_engine** out);
+void stomp_engine_destroy(stomp_engine* e);
+const char* stomp_engine_last_error(const stomp_engine* e);
+const char* stomp_last_error(void);
+
+int stomp_engine_get_theta(stomp_engine* e, double* theta);
+int stomp_engine_set_theta(stomp_engine* e, const double* theta);
+
+int stomp_engine_iterate(stomp_engine* e, int32_t iteration_number, stomp_iter_out* out);
+int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count);
+int stomp_engine_synchronize(stomp_engine* e);
+
+/* Batched Task::execute: params E x J x N, costs E x N, collision_free E,
+ * traj_out E x J x N (joint-limit-corrected free block, may be NULL).
+ * iteration_member is StompOptimizer::iteration_ (0: padding points count for the flag). */
+int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double* costs,
+                      uint8_t* collision_free, double* traj_out, int32_t iteration_member);
+
+int stomp_engine_optimize(stomp_engine* e, stomp_stats* stats, double* costs_per_iteration);
+int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj);
+int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
+
+/* Inspection for parity tests.  which: "params","noise","noise_projected"(if kept),
+ * "control_costs","probabilities" -> K_local x J x N; "state_costs" -> K_local x N. */
+int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out);
+/* which: "Rinv","L","M","Qinv" (N x N, joint selects Qinv) */
+int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, double* out);
+/* sphere world positions at the 12 padding points (12 x S x 3) */
+int stomp_engine_get_pad_positions(stomp_engine* e, double* out);
+
+/* Per-kernel device time (HIP events on the engine stream), accumulated while enabled.
+ * name: "noise", "rollout_cost", "weights", "update", "noiseless", "all". */
+int stomp_engine_set_timing(stomp_engine* e, int32_t enable);
+int stomp_engine_get_timing(stomp_engine* e, const char* name, double* total_ms, int32_t* launches);
+int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count);
+
+/* Distance-field builder (capped, quantised exact EDT):
+ *   value = sqrt(min(d2, ceil(max_expansion/res)^2)) * res
+ * d2 = integer squared cell distance to the nearest cell whose centre
+ * origin + i*res lies in an obstacle.  boxes: n_boxes x (cx,cy,cz,dx,dy,dz),
+ * axis-aligned; cylinders: n_cyl x (cx,cy,cz,radius,length), z-aligned.
+ * out_device: device buffer of nx*ny*nz floats (z fastest). */
+int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
+                    double max_expansion, const double* boxes, int32_t n_boxes, const double* cylinders,
+                    int32_t n_cylinders, float* out_device, void* stream);
+
+/* Device buffers for callers without a HIP runtime of their own (bench, tests). */
+int stomp_device_alloc(int32_t device, uint64_t bytes, void** out);
+int stomp_device_free(void* p);
+int stomp_device_copy_to_host(void* dst, const void* src, uint64_t bytes);
+int stomp_device_count(int32_t* count);
+
+/* RCCL unique id for world_size > 1 (call on rank 0, broadcast the 128 bytes). */
+int stomp_comm_unique_id(void* out128);
+
+/* deterministic math + RNG primitives evaluated on the device (parity tests) */
+int stomp_device_selftest(const double* x, int32_t n, double* out_exp, double* out_log, double* out_sin,
+                          double* out_cos, double* out_sqrt);
+int stomp_device_normals(uint64_t seed, int32_t iteration, int32_t joint, int32_t rollout, int32_t n, double* z);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,160 @@
+/*
+ * oracle/stomp_oracle.h -- TEST INFRASTRUCTURE: CPU restatement of the STOMP
+ * hot path of kalakris/stomp_motion_planner_icra2011.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ *
+ * PARITY UNPINNED: the reference cannot be compiled here (ROS rosbuild, Eigen 2,
+ * orocos KDL, boost, arm_navigation distance_field: SURVEY.md section 8c) and
+ * ships no unit tests, golden vectors or recorded outputs.  This restatement is
+ * pinned only by the reference's constants (DIFF_RULES, params.yaml), by
+ * analytic known-answer tests derived from the cited formulas, and by an
+ * independent numpy restatement (oracle/numpy_oracle.py).  See DESIGN.md.
+ *
+ * Structure follows the reference one-to-one:
+ *   so_iterate            PolicyImprovementLoop::runSingleIteration  policy_improvement_loop.cpp:143-202
+ *   so_execute            StompOptimizer::execute                    stomp_optimizer.cpp:1063-1165
+ *   so_optimize           StompOptimizer::optimize                   stomp_optimizer.cpp:249-401
+ * Build-defined choices that the reference leaves to third-party code
+ * (RNG, KDL frame conventions, distance-field lookup) are documented in
+ * DESIGN.md section "Oracle conventions".
+ */
+#ifndef STOMP_ORACLE_H
+#define STOMP_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SO_DIFF_RULE_LENGTH 7
+#define SO_NUM_DIFF_RULES 3
+#define SO_PAD (SO_DIFF_RULE_LENGTH - 1)
+
+/* One kinematic-tree segment in DFS order (parent index < own index).
+ * pose(q) = Frame(rot, trans) * Frame(Rot2(axis, q), 0)   (q_index >= 0)
+ *         = Frame(rot, trans)                              (fixed segment)
+ * frame[s] = frame[parent] * pose(q)  (treefksolverjointposaxis_partial.cpp:125, 168) */
+typedef struct {
+    int parent;       /* -1 for the root */
+    int q_index;      /* group joint index driving this segment, -1 if fixed */
+    double rot[9];    /* row-major */
+    double trans[3];
+    double axis[3];
+} so_segment;
+
+/* StompCollisionPoint (stomp_collision_point.cpp:44-55) */
+typedef struct {
+    int segment;
+    double radius;
+    double clearance;
+    double pos[3];    /* in the segment frame */
+} so_sphere;
+
+/* StompJoint limits (stomp_robot_model.cpp:158-164) */
+typedef struct {
+    int has_limits;
+    double min;
+    double max;
+    double joint_cost;  /* joint_costs/<name>, default 1.0 (stomp_optimizer.cpp:107-109) */
+} so_joint;
+
+/* Voxel grid, z fastest: value(x,y,z) = data[(x*ny + y)*nz + z] (metres, fp32) */
+typedef struct {
+    int nx, ny, nz;
+    double origin[3];
+    double resolution;
+    const float* data;
+} so_sdf;
+
+typedef struct {
+    int num_joints;             /* J */
+    int num_time_steps;         /* N (free waypoints) */
+    int num_rollouts;           /* K */
+    int num_reused_rollouts;    /* K_r */
+    int num_segments;
+    const so_segment* segments;
+    int num_spheres;
+    const so_sphere* spheres;
+    const so_joint* joints;
+    so_sdf sdf;
+    double discretization;      /* trajectory_discretization (params.yaml:5) */
+    double smoothness_costs[3]; /* vel, acc, jerk (params.yaml:8-10) */
+    double ridge_factor;
+    double smoothness_cost_weight;
+    double obstacle_cost_weight;
+    double constraint_cost_weight;
+    double torque_cost_weight;  /* must be <= 1e-9: torque term not built yet */
+    const double* noise_stddev; /* J */
+    const double* noise_decay;  /* J */
+    int use_cumulative_costs;
+    const double* start;        /* J */
+    const double* goal;         /* J */
+    uint64_t seed;
+    int max_iterations;
+    int max_iterations_after_collision_free;
+    int sum_block;              /* canonical blocked sum over rollouts (64); 0 -> 64 */
+    int dense;                  /* 1: dense N x N products exactly as the reference (CPU baseline) */
+    int threads;                /* OpenMP threads over rollouts (1 = reference) */
+} so_config;
+
+typedef struct so_problem so_problem;
+
+typedef struct {
+    double cost;                /* last_trajectory_cost_ of the noiseless rollout */
+    int collision_free;         /* last_trajectory_collision_free_ */
+} so_iter_out;
+
+typedef struct {
+    int iterations;             /* iterations run */
+    int success;
+    int success_iteration;
+    int collision_success_iteration;
+    int last_improvement_iteration;
+    double best_cost;
+} so_stats;
+
+so_problem* so_create(const so_config* cfg);
+void so_destroy(so_problem* p);
+const char* so_last_error(void);
+
+/* setup products, for stage tests; which: "Rinv","L","M","Qinv","Rall","D0","D1","D2" */
+int so_get_matrix(const so_problem* p, const char* which, int joint, double* out);
+int so_get_theta(const so_problem* p, double* theta /* J x N */);
+int so_set_theta(so_problem* p, const double* theta);
+int so_get_pad_positions(const so_problem* p, double* out /* 12 x S x 3 */);
+
+/* Task::execute on one parameter set (J x N, row per joint). iteration_member is the
+ * optimizer's iteration_ (0 => padding points count toward the collision flag). */
+int so_execute(so_problem* p, const double* params, double* costs, int* collision_free,
+               double* traj_out /* J x N clamped free block, may be NULL */, int iteration_member);
+
+/* runSingleIteration(iteration_number); the optimizer's iteration_ is iteration_number-1 */
+int so_iterate(so_problem* p, int iteration_number, so_iter_out* out);
+
+/* StompOptimizer::optimize loop (without the final torque statistics) */
+int so_optimize(so_problem* p, so_stats* stats, double* costs_per_iteration /* may be NULL */);
+int so_get_best_trajectory(const so_problem* p, double* traj /* J x N */);
+int so_get_last_trajectory(const so_problem* p, double* traj /* J x N */);
+
+/* rollout state after so_iterate, for stage tests. which:
+ * "params","noise","noise_projected","control_costs","probabilities" -> K x J x N;
+ * "state_costs" -> K x N */
+int so_get_rollouts(const so_problem* p, const char* which, double* out);
+
+/* stage primitives */
+void so_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+void so_normals(uint64_t seed, int iteration, int joint, int rollout, int n, double* z);
+double so_exp(double x);
+double so_log(double x);
+void so_sincos(double x, double* s, double* c);
+/* sphere world positions for one joint vector q (J): out S x 3 */
+int so_sphere_positions(const so_problem* p, const double* q, double* out);
+/* distance-field lookup + hinge potential for one sphere (stomp_collision_space.h:193-228) */
+double so_sdf_distance(const so_problem* p, double x, double y, double z);
+int so_potential(const so_problem* p, int sphere, const double* pos, double* potential);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,852 @@
+// engine.cpp -- host side of the C ABI in include/stomp_engine.h.
+//
+// One stomp_engine = one planning problem resident on one device: setup matrices,
+// distance field, rollout arrays and the policy theta live in HBM for the
+// engine's lifetime; an iteration is a fixed sequence of kernel launches on the
+// engine stream with no host synchronisation (stomp_engine_run), or with one
+// 9-byte read-back (stomp_engine_iterate, the runSingleIteration contract).
+#include "stomp_engine.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "setup.h"
+
+#ifdef STOMP_WITH_RCCL
+#include <rccl/rccl.h>
+#endif
+
+using namespace stomp;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse"};
+
+}  // namespace
+
+struct stomp_engine {
+    std::string err;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int J = 0, N = 0, Nall = 0, K = 0, Kr = 0, K_loc = 0, first = 0, S = 0, nseg = 0;
+    int world = 1, rank = 0;
+    uint64_t seed = 0;
+    double disc = 0.05, w_smooth = 0, w_obs = 0, w_con = 0, w_tq = 0;
+    double smooth[3] = {0, 0, 0};
+    int use_cum = 0, max_it = 0, max_it_cf = 0;
+    std::vector<double> sig_std, sig_dec, start, goal;
+    SetupOutput su;
+    DevModel model{};
+    std::vector<FkOp> ops;
+    std::vector<void*> allocs;
+    double *d_theta = nullptr, *d_LT = nullptr, *d_MT = nullptr, *d_QT = nullptr;
+    double *d_params = nullptr, *d_noise = nullptr, *d_control = nullptr, *d_prob = nullptr, *d_state = nullptr;
+    double *d_cum = nullptr, *d_u = nullptr;
+    double *d_x_params = nullptr, *d_x_noise = nullptr, *d_x_control = nullptr, *d_x_state = nullptr;
+    double *d_last_traj = nullptr, *d_best_traj = nullptr, *d_total = nullptr;
+    double *d_tmp_params = nullptr, *d_tmp_state = nullptr, *d_pad_pos = nullptr, *d_start = nullptr,
+           *d_goal = nullptr;
+    uint8_t* d_cf = nullptr;
+    float* d_sdf = nullptr;
+    int* d_pad_cf = nullptr;
+    int pad_collision = 0;
+    bool reused_next = false, extra_added = false;
+    int K_gen = 0;
+    double* h_total = nullptr;
+    uint8_t* h_cf = nullptr;
+    // eval scratch
+    int eval_cap = 0;
+    double *d_eval_params = nullptr, *d_eval_costs = nullptr, *d_eval_traj = nullptr;
+    uint8_t* d_eval_cf = nullptr;
+    // timing
+    bool timing = false;
+    struct Ev {
+        int id;
+        hipEvent_t a, b;
+    };
+    std::vector<Ev> evs;
+    std::vector<hipEvent_t> pool;
+    double tot_ms[T_COUNT] = {0};
+    int launches[T_COUNT] = {0};
+#ifdef STOMP_WITH_RCCL
+    ncclComm_t comm = nullptr;
+#endif
+};
+
+namespace {
+
+int fail(stomp_engine* e, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (e) e->err = buf;
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(e, x)                                                                          \
+    do {                                                                                       \
+        hipError_t _st = (x);                                                                  \
+        if (_st != hipSuccess)                                                                 \
+            return fail((e), STOMP_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(_st));     \
+    } while (0)
+
+template <class T>
+int dev_alloc(stomp_engine* e, T** p, size_t n)
+{
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    hipError_t st = hipMalloc(&q, n * sizeof(T));
+    if (st != hipSuccess) return fail(e, STOMP_E_DEVICE, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(st));
+    hipMemsetAsync(q, 0, n * sizeof(T), e->stream);
+    e->allocs.push_back(q);
+    *p = (T*)q;
+    return 0;
+}
+
+template <class T>
+int upload(stomp_engine* e, T** p, const T* src, size_t n)
+{
+    int rc = dev_alloc(e, p, n);
+    if (rc) return rc;
+    if (n) HIP_TRY(e, hipMemcpyAsync(*p, src, n * sizeof(T), hipMemcpyHostToDevice, e->stream));
+    return 0;
+}
+
+hipEvent_t get_event(stomp_engine* e)
+{
+    if (!e->pool.empty()) {
+        hipEvent_t ev = e->pool.back();
+        e->pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev;
+    hipEventCreate(&ev);
+    return ev;
+}
+
+struct Timed {
+    stomp_engine* e;
+    int id;
+    hipEvent_t a = nullptr, b = nullptr;
+    Timed(stomp_engine* e_, int id_) : e(e_), id(id_)
+    {
+        if (e->timing) {
+            a = get_event(e);
+            b = get_event(e);
+            hipEventRecord(a, e->stream);
+        }
+    }
+    ~Timed()
+    {
+        if (e->timing) {
+            hipEventRecord(b, e->stream);
+            e->evs.push_back({id, a, b});
+        }
+    }
+};
+
+void collect_timing(stomp_engine* e)
+{
+    if (e->evs.empty()) return;
+    hipStreamSynchronize(e->stream);
+    for (auto& v : e->evs) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, v.a, v.b);
+        e->tot_ms[v.id] += ms;
+        e->launches[v.id] += 1;
+        e->pool.push_back(v.a);
+        e->pool.push_back(v.b);
+    }
+    e->evs.clear();
+}
+
+// FK program: frames of the segments that carry spheres or are their ancestors, in
+// DFS order, each composed from its parent's live slot; sphere runs emitted in list
+// order right after their segment's frame (requires sphere segments non-decreasing).
+int plan_fk(stomp_engine* e, const stomp_engine_desc* d, std::vector<FkOp>& ops)
+{
+    const int ns = d->num_segments;
+    std::vector<char> needed(ns, 0);
+    int prev = -1;
+    for (int j = 0; j < d->num_spheres; ++j) {
+        int s = d->spheres[j].segment;
+        if (s < prev)
+            return fail(e, STOMP_E_UNSUPPORTED,
+                        "sphere list must be ordered by segment (sphere %d on segment %d after segment %d)", j, s, prev);
+        prev = s;
+        for (int a = s; a >= 0 && !needed[a]; a = d->segments[a].parent) needed[a] = 1;
+    }
+    std::vector<int> remaining(ns, 0), slot_of(ns, -1);
+    for (int s = 0; s < ns; ++s)
+        if (needed[s] && d->segments[s].parent >= 0) remaining[d->segments[s].parent]++;
+    bool used[kSlots] = {false, false, false, false};
+    auto alloc = [&]() {
+        for (int k = 0; k < kSlots; ++k)
+            if (!used[k]) { used[k] = true; return k; }
+        return -1;
+    };
+    int sph = 0;
+    for (int s = 0; s < ns; ++s) {
+        if (!needed[s]) continue;
+        const int p = d->segments[s].parent;
+        int from = p >= 0 ? slot_of[p] : -1, to;
+        if (p >= 0 && --remaining[p] == 0) {
+            to = from;   // parent frame dead after this child: overwrite in place
+            slot_of[p] = -1;
+        } else {
+            to = alloc();
+            if (to < 0) return fail(e, STOMP_E_UNSUPPORTED, "kinematic tree needs more than %d live frames", kSlots);
+        }
+        slot_of[s] = to;
+        int b = sph;
+        while (sph < d->num_spheres && d->spheres[sph].segment == s) ++sph;
+        bool first = true;
+        for (int a = b; a < sph || first; a += kRunMax) {
+            FkOp o;
+            o.seg = first ? s : -1;
+            o.from = first ? from : to;
+            o.to = to;
+            o.sph_begin = std::min(a, sph);
+            o.sph_end = std::min(a + kRunMax, sph);
+            ops.push_back(o);
+            first = false;
+        }
+        if (remaining[s] == 0) {
+            used[to] = false;
+            slot_of[s] = -1;
+        }
+    }
+    return 0;
+}
+
+void release(stomp_engine* e)
+{
+    if (!e) return;
+    if (e->stream) hipStreamSynchronize(e->stream);
+    for (auto& v : e->evs) { hipEventDestroy(v.a); hipEventDestroy(v.b); }
+    for (auto ev : e->pool) hipEventDestroy(ev);
+    for (void* p : e->allocs) hipFree(p);
+    if (e->h_total) hipHostFree(e->h_total);
+    if (e->h_cf) hipHostFree(e->h_cf);
+#ifdef STOMP_WITH_RCCL
+    if (e->comm) ncclCommDestroy(e->comm);
+#endif
+    if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
+}
+
+int enqueue_iteration(stomp_engine* e, int it)
+{
+    const int member = it - 1;
+    NoiseArgs na{};
+    na.J = e->J; na.N = e->N; na.Nall = e->Nall; na.K_loc = e->K_loc; na.first_global = e->first;
+    na.iteration = it; na.seed = e->seed;
+    for (int d = 0; d < e->J; ++d) na.sigma.v[d] = e->sig_std[d] * std::pow(e->sig_dec[d], it - 1);
+    na.theta = e->d_theta; na.LT = e->d_LT; na.MT = e->d_MT; na.start = e->d_start; na.goal = e->d_goal;
+    std::memcpy(na.dcoef, e->su.dcoef, sizeof na.dcoef);
+    const double w = 0.5 * e->w_smooth;   // policy_improvement.cpp:487
+    for (int r = 0; r < 3; ++r) na.wr[r] = w * e->smooth[r];
+    na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0;
+
+    // generateRollouts bookkeeping (policy_improvement.cpp:167-175)
+    e->K_gen = e->K - e->Kr;
+    if (!e->reused_next) {
+        e->K_gen = e->K;
+        if (e->Kr > 0) e->reused_next = true;
+    } else {
+        Timed tm(e, T_REUSE);
+        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, e->extra_added ? 1 : 0, e->d_params, e->d_noise, e->d_state,
+                     e->d_control, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params,
+                     e->d_tmp_state, e->stream);
+        e->extra_added = false;
+    }
+    na.K_gen_global = e->K_gen;
+    {
+        Timed tm(e, T_NOISE);
+        launch_noise(na, 4, e->stream);
+    }
+    // Task::execute for the generated rollouts of this shard
+    int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
+    if (g1 > g0) {
+        Timed tm(e, T_COST);
+        launch_rollout_cost(e->model, e->d_params, (long long)e->J * e->N, g1 - g0, e->d_state, nullptr, nullptr,
+                            nullptr, member, e->stream);
+    }
+    WeightArgs wa{};
+    wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
+    wa.state = e->d_state; wa.control = e->d_control; wa.noise = e->d_noise;
+    wa.cum = nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
+    {
+        Timed tm(e, T_WEIGHTS);
+        if (e->use_cum) {
+            wa.cum = e->d_cum;
+            launch_cumulative(wa, e->stream);
+        }
+        launch_weights(wa, e->stream);
+    }
+    {
+        Timed tm(e, T_UPDATE);
+        launch_update(e->J, e->N, e->d_MT, e->d_u, e->d_theta, e->stream);
+    }
+    {
+        Timed tm(e, T_NOISELESS);
+        launch_rollout_cost(e->model, e->d_theta, 0, 1, e->d_x_state, e->d_cf, e->d_last_traj, e->d_total, member,
+                            e->stream);
+    }
+    if (e->Kr > 0) {
+        // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0
+        hipMemcpyAsync(e->d_x_params, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToDevice, e->stream);
+        NoiseArgs xa = na;
+        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 1;
+        xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
+        launch_noise(xa, 1, e->stream);
+        e->extra_added = true;
+    }
+    hipError_t st = hipGetLastError();
+    if (st != hipSuccess) return fail(e, STOMP_E_DEVICE, "kernel launch failed: %s", hipGetErrorString(st));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* stomp_last_error(void) { return g_last_error.c_str(); }
+
+const char* stomp_engine_last_error(const stomp_engine* e) { return e ? e->err.c_str() : g_last_error.c_str(); }
+
+int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
+{
+    if (!d || !out) return fail(nullptr, STOMP_E_INVALID, "null argument");
+    *out = nullptr;
+    if (d->abi_version != STOMP_ENGINE_ABI_VERSION)
+        return fail(nullptr, STOMP_E_INVALID, "abi_version %d != %d", d->abi_version, STOMP_ENGINE_ABI_VERSION);
+    if (d->num_joints <= 0 || d->num_joints > kMaxJoints)
+        return fail(nullptr, STOMP_E_INVALID, "num_joints must be in [1, %d]", kMaxJoints);
+    if (d->num_time_steps <= 0 || d->num_time_steps > 256)
+        return fail(nullptr, STOMP_E_INVALID, "num_time_steps must be in [1, 256]");
+    if (d->num_rollouts <= 0) return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be positive");
+    if (d->num_reused_rollouts < 0 || d->num_reused_rollouts >= d->num_rollouts)
+        return fail(nullptr, STOMP_E_INVALID, "Number of reused rollouts must be strictly less than number of rollouts.");
+    if (d->torque_cost_weight > 1e-9)
+        return fail(nullptr, STOMP_E_UNSUPPORTED, "torque cost (stomp_optimizer.cpp:1120-1142) is not built yet");
+    if (d->num_segments <= 0 || !d->segments || (d->num_spheres > 0 && !d->spheres) || !d->joints || !d->noise_stddev ||
+        !d->noise_decay || !d->start || !d->goal || !d->grid.data)
+        return fail(nullptr, STOMP_E_INVALID, "missing table pointer");
+    if (d->grid.nx < 3 || d->grid.ny < 3 || d->grid.nz < 3 || !(d->grid.resolution > 0))
+        return fail(nullptr, STOMP_E_INVALID, "invalid grid");
+    for (int s = 0; s < d->num_segments; ++s)
+        if (d->segments[s].parent >= s || d->segments[s].q_index >= d->num_joints)
+            return fail(nullptr, STOMP_E_INVALID, "segment %d: parent must precede it (DFS order), q_index < J", s);
+    for (int j = 0; j < d->num_spheres; ++j)
+        if (d->spheres[j].segment < 0 || d->spheres[j].segment >= d->num_segments)
+            return fail(nullptr, STOMP_E_INVALID, "sphere %d: bad segment", j);
+    const int world = d->world_size > 0 ? d->world_size : 1;
+    if (world > 1) {
+        if (d->num_reused_rollouts > 0)
+            return fail(nullptr, STOMP_E_UNSUPPORTED, "rollout reuse is single-device only");
+        if (d->num_rollouts % (world * kSumBlock) != 0)
+            return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be a multiple of 64 * world_size");
+#ifndef STOMP_WITH_RCCL
+        return fail(nullptr, STOMP_E_UNSUPPORTED, "built without RCCL");
+#endif
+    }
+
+    stomp_engine* e = new stomp_engine();
+    e->device = d->device;
+    int rc;
+    if (hipSetDevice(d->device) != hipSuccess) {
+        rc = fail(nullptr, STOMP_E_DEVICE, "hipSetDevice(%d) failed", d->device);
+        delete e;
+        return rc;
+    }
+    if (d->stream) {
+        e->stream = (hipStream_t)d->stream;
+    } else {
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+        e->own_stream = true;
+    }
+    e->J = d->num_joints; e->N = d->num_time_steps; e->Nall = e->N + 2 * kPad;
+    e->K = d->num_rollouts; e->Kr = d->num_reused_rollouts;
+    e->world = world; e->rank = world > 1 ? d->rank : 0;
+    e->K_loc = e->K / world; e->first = e->rank * e->K_loc;
+    if (e->K_loc > kSumBlock * 64) {
+        rc = fail(e, STOMP_E_INVALID, "at most %d rollouts per device", kSumBlock * 64);
+        g_last_error = e->err; release(e); delete e; return rc;
+    }
+    e->S = d->num_spheres; e->nseg = d->num_segments; e->seed = d->seed;
+    e->disc = d->discretization; e->w_smooth = d->smoothness_cost_weight; e->w_obs = d->obstacle_cost_weight;
+    e->w_con = d->constraint_cost_weight; e->w_tq = d->torque_cost_weight;
+    for (int r = 0; r < 3; ++r) e->smooth[r] = d->smoothness_costs[r];
+    e->use_cum = d->use_cumulative_costs; e->max_it = d->max_iterations;
+    e->max_it_cf = d->max_iterations_after_collision_free;
+    e->sig_std.assign(d->noise_stddev, d->noise_stddev + e->J);
+    e->sig_dec.assign(d->noise_decay, d->noise_decay + e->J);
+    e->start.assign(d->start, d->start + e->J);
+    e->goal.assign(d->goal, d->goal + e->J);
+
+#define CREATE_TRY(x)                           \
+    do {                                        \
+        if ((rc = (x)) != 0) {                  \
+            g_last_error = e->err;              \
+            release(e);                         \
+            delete e;                           \
+            return rc;                          \
+        }                                       \
+    } while (0)
+
+    CREATE_TRY(plan_fk(e, d, e->ops));
+    SetupInput si;
+    si.J = e->J; si.N = e->N; si.discretization = e->disc;
+    for (int r = 0; r < 3; ++r) si.smoothness_costs[r] = e->smooth[r];
+    si.ridge_factor = d->ridge_factor;
+    for (int j = 0; j < e->J; ++j) si.joint_cost.push_back(d->joints[j].joint_cost);
+    si.start = e->start; si.goal = e->goal;
+    std::string msg = compute_setup(si, e->su);
+    if (!msg.empty()) CREATE_TRY(fail(e, STOMP_E_INVALID, "%s", msg.c_str()));
+
+    const int J = e->J, N = e->N;
+    std::vector<double> LT((size_t)N * N), MT((size_t)N * N), QT((size_t)J * N * N);
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < N; ++k) {
+            LT[(size_t)k * N + i] = e->su.L[(size_t)i * N + k];
+            MT[(size_t)k * N + i] = e->su.M[(size_t)i * N + k];
+        }
+    for (int j = 0; j < J; ++j)
+        for (int i = 0; i < N; ++i)
+            for (int k = 0; k < N; ++k)
+                QT[((size_t)j * N + k) * N + i] = e->su.Qinv[((size_t)j * N + i) * N + k];
+    std::vector<DevSegment> segs(e->nseg);
+    for (int s = 0; s < e->nseg; ++s) {
+        const stomp_segment& g = d->segments[s];
+        segs[s].parent = g.parent; segs[s].q_index = g.q_index;
+        std::memcpy(segs[s].rot, g.rot, sizeof g.rot);
+        std::memcpy(segs[s].trans, g.trans, sizeof g.trans);
+        std::memcpy(segs[s].axis, g.axis, sizeof g.axis);
+    }
+    std::vector<DevSphere> sph(std::max(e->S, 1));
+    for (int j = 0; j < e->S; ++j) {
+        const stomp_sphere& g = d->spheres[j];
+        sph[j].segment = g.segment; sph[j].pad_ = 0;
+        sph[j].radius = g.radius; sph[j].clearance = g.clearance;
+        sph[j].inv_clearance = 1.0 / g.clearance;   // stomp_collision_point.cpp:50
+        std::memcpy(sph[j].pos, g.pos, sizeof g.pos);
+    }
+    std::vector<int> has_lim(J);
+    std::vector<double> jmin(J), jmax(J);
+    for (int j = 0; j < J; ++j) {
+        has_lim[j] = d->joints[j].has_limits;
+        jmin[j] = d->joints[j].min;
+        jmax[j] = d->joints[j].max;
+    }
+    DevSegment* d_segs; DevSphere* d_sph; FkOp* d_ops; int* d_hl; double *d_jmin, *d_jmax;
+    CREATE_TRY(upload(e, &d_segs, segs.data(), segs.size()));
+    CREATE_TRY(upload(e, &d_sph, sph.data(), sph.size()));
+    CREATE_TRY(upload(e, &d_ops, e->ops.data(), e->ops.size()));
+    CREATE_TRY(upload(e, &d_hl, has_lim.data(), has_lim.size()));
+    CREATE_TRY(upload(e, &d_jmin, jmin.data(), jmin.size()));
+    CREATE_TRY(upload(e, &d_jmax, jmax.data(), jmax.size()));
+    CREATE_TRY(upload(e, &e->d_QT, QT.data(), QT.size()));
+    CREATE_TRY(upload(e, &e->d_LT, LT.data(), LT.size()));
+    CREATE_TRY(upload(e, &e->d_MT, MT.data(), MT.size()));
+    CREATE_TRY(upload(e, &e->d_theta, e->su.theta.data(), e->su.theta.size()));
+    CREATE_TRY(upload(e, &e->d_start, e->start.data(), e->start.size()));
+    CREATE_TRY(upload(e, &e->d_goal, e->goal.data(), e->goal.size()));
+    const size_t ncell = (size_t)d->grid.nx * d->grid.ny * d->grid.nz;
+    if (d->grid.data_on_device) {
+        e->d_sdf = (float*)d->grid.data;
+    } else {
+        CREATE_TRY(upload(e, &e->d_sdf, d->grid.data, ncell));
+    }
+    const size_t KJN = (size_t)e->K_loc * J * N;
+    CREATE_TRY(dev_alloc(e, &e->d_params, KJN));
+    CREATE_TRY(dev_alloc(e, &e->d_noise, KJN));
+    CREATE_TRY(dev_alloc(e, &e->d_control, KJN));
+    CREATE_TRY(dev_alloc(e, &e->d_prob, KJN));
+    CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
+    if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
+    CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_x_params, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_x_noise, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_x_control, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_x_state, (size_t)N));
+    CREATE_TRY(dev_alloc(e, &e->d_last_traj, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_best_traj, (size_t)J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_total, 1));
+    CREATE_TRY(dev_alloc(e, &e->d_cf, 1));
+    CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
+    CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
+    CREATE_TRY(dev_alloc(e, &e->d_pad_pos, (size_t)12 * std::max(e->S, 1) * 3));
+    CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
+    if (hipHostMalloc((void**)&e->h_total, sizeof(double)) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_cf, 16) != hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
+
+    DevModel& m = e->model;
+    m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size();
+    m.segs = d_segs; m.sph = d_sph; m.ops = d_ops; m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
+    m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
+    m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
+    m.start = e->d_start; m.goal = e->d_goal;
+    const double invTime = 1.0 / e->disc;   // stomp_optimizer.cpp:620
+    for (int k = 0; k < 7; ++k) m.vel_coef[k] = invTime * kDiffRules[0][k];
+    m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
+    m.has_limits = d_hl; m.jmin = d_jmin; m.jmax = d_jmax; m.QT = e->d_QT;
+    m.pad_collision = 0;
+    launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
+    int pad_cf = 0;
+    if (hipMemcpyAsync(&pad_cf, e->d_pad_cf, sizeof(int), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "padding FK failed: %s", hipGetErrorString(hipGetLastError())));
+    m.pad_collision = pad_cf;
+    e->pad_collision = pad_cf;
+    hipMemcpyAsync(e->d_last_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
+    hipMemcpyAsync(e->d_best_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
+
+#ifdef STOMP_WITH_RCCL
+    if (world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, d->comm_id, sizeof id);
+        if (ncclCommInitRank(&e->comm, world, id, e->rank) != ncclSuccess)
+            CREATE_TRY(fail(e, STOMP_E_COMM, "ncclCommInitRank failed"));
+    }
+#endif
+    if (hipStreamSynchronize(e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "setup failed"));
+    *out = e;
+    return 0;
+#undef CREATE_TRY
+}
+
+void stomp_engine_destroy(stomp_engine* e)
+{
+    release(e);
+    delete e;
+}
+
+int stomp_engine_get_theta(stomp_engine* e, double* theta)
+{
+    HIP_TRY(e, hipMemcpyAsync(theta, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_set_theta(stomp_engine* e, const double* theta)
+{
+    HIP_TRY(e, hipMemcpyAsync(e->d_theta, theta, sizeof(double) * e->J * e->N, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
+{
+    int rc = enqueue_iteration(e, it);
+    if (rc) return rc;
+    HIP_TRY(e, hipMemcpyAsync(e->h_total, e->d_total, sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->h_cf, e->d_cf, 1, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (out) {
+        out->cost = *e->h_total;
+        out->collision_free = e->h_cf[0];
+    }
+    return 0;
+}
+
+int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count)
+{
+    for (int i = 0; i < count; ++i) {
+        int rc = enqueue_iteration(e, first_iteration + i);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int stomp_engine_synchronize(stomp_engine* e)
+{
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double* costs, uint8_t* collision_free,
+                      double* traj_out, int32_t iteration_member)
+{
+    if (num <= 0) return 0;
+    const size_t JN = (size_t)e->J * e->N;
+    if (num > e->eval_cap) {
+        for (void* p : {(void*)e->d_eval_params, (void*)e->d_eval_costs, (void*)e->d_eval_traj, (void*)e->d_eval_cf}) {
+            if (!p) continue;
+            hipFree(p);
+            e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), p), e->allocs.end());
+        }
+        int rc;
+        if ((rc = dev_alloc(e, &e->d_eval_params, num * JN))) return rc;
+        if ((rc = dev_alloc(e, &e->d_eval_costs, (size_t)num * e->N))) return rc;
+        if ((rc = dev_alloc(e, &e->d_eval_traj, num * JN))) return rc;
+        if ((rc = dev_alloc(e, &e->d_eval_cf, (size_t)num))) return rc;
+        e->eval_cap = num;
+    }
+    HIP_TRY(e, hipMemcpyAsync(e->d_eval_params, params, sizeof(double) * num * JN, hipMemcpyHostToDevice, e->stream));
+    launch_rollout_cost(e->model, e->d_eval_params, (long long)JN, num, e->d_eval_costs, e->d_eval_cf,
+                        traj_out ? e->d_eval_traj : nullptr, nullptr, iteration_member, e->stream);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipMemcpyAsync(costs, e->d_eval_costs, sizeof(double) * num * e->N, hipMemcpyDeviceToHost, e->stream));
+    if (collision_free)
+        HIP_TRY(e, hipMemcpyAsync(collision_free, e->d_eval_cf, num, hipMemcpyDeviceToHost, e->stream));
+    if (traj_out)
+        HIP_TRY(e, hipMemcpyAsync(traj_out, e->d_eval_traj, sizeof(double) * num * JN, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// StompOptimizer::optimize loop (stomp_optimizer.cpp:284-359), one read-back per iteration
+int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it)
+{
+    stomp_stats s;
+    s.collision_success_iteration = -1;
+    s.success_iteration = -1;
+    s.success = 0;
+    s.last_improvement_iteration = -1;
+    int cfi = 0, it;
+    double best = 0.0;
+    const size_t bytes = sizeof(double) * e->J * e->N;
+    for (it = 0; it < e->max_it; it++) {
+        stomp_iter_out o;
+        int rc = stomp_engine_iterate(e, it + 1, &o);
+        if (rc) return rc;
+        if (o.collision_free) cfi++;
+        else cfi = 0;
+        if (o.collision_free && s.collision_success_iteration == -1) s.collision_success_iteration = it;
+        if (o.collision_free && s.success_iteration == -1) {
+            s.success_iteration = it;
+            s.success = 1;
+        }
+        if (costs_per_it) costs_per_it[it] = o.cost;
+        if (it == 0 || (o.cost < best && o.collision_free)) {
+            HIP_TRY(e, hipMemcpyAsync(e->d_best_traj, e->d_last_traj, bytes, hipMemcpyDeviceToDevice, e->stream));
+            best = o.cost;
+            if (it != 0) s.last_improvement_iteration = it;
+        }
+        if (cfi >= e->max_it_cf) {
+            it++;
+            break;
+        }
+    }
+    s.iterations = it;
+    s.best_cost = best;
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (st) *st = s;
+    return 0;
+}
+
+int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
+{
+    HIP_TRY(e, hipMemcpyAsync(traj, e->d_best_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj)
+{
+    HIP_TRY(e, hipMemcpyAsync(traj, e->d_last_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
+{
+    const size_t KJN = (size_t)e->K_loc * e->J * e->N;
+    const double* src = nullptr;
+    size_t n = KJN;
+    if (!std::strcmp(which, "params")) src = e->d_params;
+    else if (!std::strcmp(which, "noise")) src = e->d_noise;
+    else if (!std::strcmp(which, "control_costs")) src = e->d_control;
+    else if (!std::strcmp(which, "probabilities")) src = e->d_prob;
+    else if (!std::strcmp(which, "state_costs")) { src = e->d_state; n = (size_t)e->K_loc * e->N; }
+    else return fail(e, STOMP_E_INVALID, "unknown rollout field '%s'", which);
+    HIP_TRY(e, hipMemcpyAsync(out, src, n * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, double* out)
+{
+    const size_t NN = (size_t)e->N * e->N;
+    if (!std::strcmp(which, "Rinv")) std::memcpy(out, e->su.Rinv.data(), NN * 8);
+    else if (!std::strcmp(which, "L")) std::memcpy(out, e->su.L.data(), NN * 8);
+    else if (!std::strcmp(which, "M")) std::memcpy(out, e->su.M.data(), NN * 8);
+    else if (!std::strcmp(which, "Qinv")) {
+        if (joint < 0 || joint >= e->J) return fail(e, STOMP_E_INVALID, "joint out of range");
+        std::memcpy(out, e->su.Qinv.data() + (size_t)joint * NN, NN * 8);
+    } else return fail(e, STOMP_E_INVALID, "unknown matrix '%s'", which);
+    return 0;
+}
+
+int stomp_engine_get_pad_positions(stomp_engine* e, double* out)
+{
+    HIP_TRY(e, hipMemcpyAsync(out, e->d_pad_pos, sizeof(double) * 12 * e->S * 3, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_engine_set_timing(stomp_engine* e, int32_t enable)
+{
+    collect_timing(e);
+    e->timing = enable != 0;
+    for (int i = 0; i < T_COUNT; ++i) { e->tot_ms[i] = 0; e->launches[i] = 0; }
+    return 0;
+}
+
+int stomp_engine_get_timing(stomp_engine* e, const char* name, double* total_ms, int32_t* launches)
+{
+    collect_timing(e);
+    double t = 0;
+    int n = 0;
+    bool found = false;
+    for (int i = 0; i < T_COUNT; ++i)
+        if (!std::strcmp(name, "all") || !std::strcmp(name, kTimerNames[i])) {
+            t += e->tot_ms[i];
+            n += e->launches[i];
+            found = true;
+        }
+    if (!found) return fail(e, STOMP_E_INVALID, "unknown timer '%s'", name);
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = n;
+    return 0;
+}
+
+int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
+{
+    if (first) *first = e->first;
+    if (count) *count = e->K_loc;
+    return 0;
+}
+
+int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double res, double max_expansion,
+                    const double* boxes, int32_t n_boxes, const double* cyl, int32_t n_cyl, float* out, void* stream)
+{
+    if (nx <= 0 || ny <= 0 || nz <= 0 || !(res > 0) || !out) return fail(nullptr, STOMP_E_INVALID, "invalid grid");
+    const int n[3] = {nx, ny, nz};
+    const int cap = (int)std::ceil(max_expansion / res);
+    const int cap2 = cap * cap;
+    auto range = [&](double lo, double hi, int a, int& i0, int& i1) {
+        i0 = std::max((int)std::ceil((lo - origin[a]) / res), 0);
+        i1 = std::min((int)std::floor((hi - origin[a]) / res), n[a] - 1);
+    };
+    std::vector<int> br;
+    for (int b = 0; b < n_boxes; ++b) {
+        const double* q = boxes + 6 * b;
+        int r[6];
+        bool empty = false;
+        for (int a = 0; a < 3; ++a) {
+            range(q[a] - q[3 + a] / 2.0, q[a] + q[3 + a] / 2.0, a, r[2 * a], r[2 * a + 1]);
+            if (r[2 * a] > r[2 * a + 1]) empty = true;
+        }
+        if (!empty) br.insert(br.end(), r, r + 6);
+    }
+    const long long big = 1LL << 40;
+    std::vector<long long> cd2;
+    std::vector<int> cz;
+    for (int c = 0; c < n_cyl; ++c) {
+        const double* q = cyl + 5 * c;
+        int z0, z1;
+        range(q[2] - q[4] / 2.0, q[2] + q[4] / 2.0, 2, z0, z1);
+        if (z0 > z1) continue;
+        std::vector<std::pair<int, int>> disc;
+        for (int i = 0; i < nx; ++i) {
+            const double xs = origin[0] + i * res - q[0];
+            for (int j = 0; j < ny; ++j) {
+                const double ys = origin[1] + j * res - q[1];
+                if (xs * xs + ys * ys <= q[3] * q[3]) disc.push_back({i, j});
+            }
+        }
+        if (disc.empty()) continue;
+        std::vector<long long> t((size_t)nx * ny, big);
+        for (int i = 0; i < nx; ++i)
+            for (int j = 0; j < ny; ++j) {
+                long long best = big;
+                for (auto& pq : disc) {
+                    long long dx = i - pq.first, dy = j - pq.second;
+                    long long v = dx * dx + dy * dy;
+                    if (v < best) best = v;
+                }
+                t[(size_t)i * ny + j] = std::min(best, (long long)cap2);
+            }
+        cd2.insert(cd2.end(), t.begin(), t.end());
+        cz.push_back(z0);
+        cz.push_back(z1);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    int* d_b = nullptr;
+    long long* d_c = nullptr;
+    int* d_z = nullptr;
+    if (!br.empty() && hipMalloc(&d_b, br.size() * sizeof(int)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
+    if (!cd2.empty() && hipMalloc(&d_c, cd2.size() * sizeof(long long)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
+    if (!cz.empty() && hipMalloc(&d_z, cz.size() * sizeof(int)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
+    if (d_b) hipMemcpyAsync(d_b, br.data(), br.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    if (d_c) hipMemcpyAsync(d_c, cd2.data(), cd2.size() * sizeof(long long), hipMemcpyHostToDevice, s);
+    if (d_z) hipMemcpyAsync(d_z, cz.data(), cz.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    launch_sdf_build(nx, ny, nz, cap2, res, d_b, (int)br.size() / 6, d_c, d_z, (int)cz.size() / 2, out, s);
+    hipError_t st = hipStreamSynchronize(s);
+    if (d_b) hipFree(d_b);
+    if (d_c) hipFree(d_c);
+    if (d_z) hipFree(d_z);
+    if (st != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(st));
+    return 0;
+}
+
+int stomp_device_alloc(int32_t device, uint64_t bytes, void** out)
+{
+    if (hipSetDevice(device) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipSetDevice(%d) failed", device);
+    hipError_t st = hipMalloc(out, bytes ? bytes : 1);
+    if (st != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc: %s", hipGetErrorString(st));
+    return 0;
+}
+
+int stomp_device_free(void* p)
+{
+    hipError_t st = hipFree(p);
+    return st == hipSuccess ? 0 : fail(nullptr, STOMP_E_DEVICE, "hipFree: %s", hipGetErrorString(st));
+}
+
+int stomp_device_copy_to_host(void* dst, const void* src, uint64_t bytes)
+{
+    hipError_t st = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    return st == hipSuccess ? 0 : fail(nullptr, STOMP_E_DEVICE, "hipMemcpy: %s", hipGetErrorString(st));
+}
+
+int stomp_device_count(int32_t* count)
+{
+    int n = 0;
+    hipError_t st = hipGetDeviceCount(&n);
+    *count = st == hipSuccess ? n : 0;
+    return 0;
+}
+
+int stomp_comm_unique_id(void* out128)
+{
+#ifdef STOMP_WITH_RCCL
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return fail(nullptr, STOMP_E_COMM, "ncclGetUniqueId failed");
+    std::memcpy(out128, &id, sizeof id);
+    return 0;
+#else
+    (void)out128;
+    return fail(nullptr, STOMP_E_UNSUPPORTED, "built without RCCL");
+#endif
+}
+
+}  // extern "C"

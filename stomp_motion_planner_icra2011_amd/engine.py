@@ -1,0 +1,346 @@
+"""ctypes binding of the C ABI in include/stomp_engine.h (libstomp_engine.so, built in-tree).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded the
+constructor raises.  The CPU oracle lives under oracle/ and is test-only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import _build
+
+_LIB_PATH = _build.LIB
+ABI_VERSION = 1
+
+
+class stomp_segment(C.Structure):
+    _fields_ = [("parent", C.c_int32), ("q_index", C.c_int32), ("rot", C.c_double * 9),
+                ("trans", C.c_double * 3), ("axis", C.c_double * 3)]
+
+
+class stomp_sphere(C.Structure):
+    _fields_ = [("segment", C.c_int32), ("radius", C.c_double), ("clearance", C.c_double), ("pos", C.c_double * 3)]
+
+
+class stomp_joint(C.Structure):
+    _fields_ = [("has_limits", C.c_int32), ("min", C.c_double), ("max", C.c_double), ("joint_cost", C.c_double)]
+
+
+class stomp_grid(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("nz", C.c_int32), ("origin", C.c_double * 3),
+                ("resolution", C.c_double), ("data", C.c_void_p), ("data_on_device", C.c_int32)]
+
+
+class stomp_engine_desc(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("num_joints", C.c_int32), ("num_time_steps", C.c_int32),
+                ("num_rollouts", C.c_int32), ("num_reused_rollouts", C.c_int32), ("num_segments", C.c_int32),
+                ("segments", C.POINTER(stomp_segment)), ("num_spheres", C.c_int32),
+                ("spheres", C.POINTER(stomp_sphere)), ("joints", C.POINTER(stomp_joint)), ("grid", stomp_grid),
+                ("discretization", C.c_double), ("smoothness_costs", C.c_double * 3), ("ridge_factor", C.c_double),
+                ("smoothness_cost_weight", C.c_double), ("obstacle_cost_weight", C.c_double),
+                ("constraint_cost_weight", C.c_double), ("torque_cost_weight", C.c_double),
+                ("noise_stddev", C.POINTER(C.c_double)), ("noise_decay", C.POINTER(C.c_double)),
+                ("use_cumulative_costs", C.c_int32), ("start", C.POINTER(C.c_double)),
+                ("goal", C.POINTER(C.c_double)), ("seed", C.c_uint64), ("max_iterations", C.c_int32),
+                ("max_iterations_after_collision_free", C.c_int32), ("device", C.c_int32), ("stream", C.c_void_p),
+                ("rank", C.c_int32), ("world_size", C.c_int32), ("comm_id", C.c_void_p)]
+
+
+class stomp_iter_out(C.Structure):
+    _fields_ = [("cost", C.c_double), ("collision_free", C.c_int32)]
+
+
+class stomp_stats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("success", C.c_int32), ("success_iteration", C.c_int32),
+                ("collision_success_iteration", C.c_int32), ("last_improvement_iteration", C.c_int32),
+                ("best_cost", C.c_double)]
+
+
+# every symbol include/stomp_engine.h declares (checked by tests/test_abi.py)
+EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_error", "stomp_last_error",
+            "stomp_engine_get_theta", "stomp_engine_set_theta", "stomp_engine_iterate", "stomp_engine_run",
+            "stomp_engine_synchronize", "stomp_engine_eval", "stomp_engine_optimize",
+            "stomp_engine_get_best_trajectory", "stomp_engine_get_last_trajectory", "stomp_engine_get_rollouts",
+            "stomp_engine_get_matrix", "stomp_engine_get_pad_positions", "stomp_engine_set_timing",
+            "stomp_engine_get_timing", "stomp_engine_local_rollouts", "stomp_sdf_build", "stomp_comm_unique_id",
+            "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
+            "stomp_device_copy_to_host", "stomp_device_count"]
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None):
+    """Loads libstomp_engine.so (building it first if absent and hipcc is available)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or _LIB_PATH
+    if not os.path.exists(path):
+        if os.path.exists(_build.HIPCC):
+            _build.build()
+        else:
+            raise RuntimeError(f"STOMP HIP engine library missing: {path} (run __graft_entry__.build())")
+    l = C.CDLL(path)
+    P, dp = C.c_void_p, C.POINTER(C.c_double)
+    l.stomp_engine_create.argtypes = [C.POINTER(stomp_engine_desc), C.POINTER(C.c_void_p)]
+    l.stomp_engine_destroy.argtypes = [P]
+    l.stomp_engine_last_error.restype = C.c_char_p
+    l.stomp_engine_last_error.argtypes = [P]
+    l.stomp_last_error.restype = C.c_char_p
+    l.stomp_engine_get_theta.argtypes = [P, dp]
+    l.stomp_engine_set_theta.argtypes = [P, dp]
+    l.stomp_engine_iterate.argtypes = [P, C.c_int32, C.POINTER(stomp_iter_out)]
+    l.stomp_engine_run.argtypes = [P, C.c_int32, C.c_int32]
+    l.stomp_engine_synchronize.argtypes = [P]
+    l.stomp_engine_eval.argtypes = [P, dp, C.c_int32, dp, C.POINTER(C.c_uint8), dp, C.c_int32]
+    l.stomp_engine_optimize.argtypes = [P, C.POINTER(stomp_stats), dp]
+    l.stomp_engine_get_best_trajectory.argtypes = [P, dp]
+    l.stomp_engine_get_last_trajectory.argtypes = [P, dp]
+    l.stomp_engine_get_rollouts.argtypes = [P, C.c_char_p, dp]
+    l.stomp_engine_get_matrix.argtypes = [P, C.c_char_p, C.c_int32, dp]
+    l.stomp_engine_get_pad_positions.argtypes = [P, dp]
+    l.stomp_engine_set_timing.argtypes = [P, C.c_int32]
+    l.stomp_engine_get_timing.argtypes = [P, C.c_char_p, dp, C.POINTER(C.c_int32)]
+    l.stomp_engine_local_rollouts.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    l.stomp_sdf_build.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double, dp, C.c_int32, dp,
+                                  C.c_int32, C.c_void_p, C.c_void_p]
+    l.stomp_comm_unique_id.argtypes = [C.c_void_p]
+    l.stomp_device_alloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
+    l.stomp_device_free.argtypes = [C.c_void_p]
+    l.stomp_device_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    l.stomp_device_count.argtypes = [C.POINTER(C.c_int32)]
+    l.stomp_device_selftest.argtypes = [dp, C.c_int32, dp, dp, dp, dp, dp]
+    l.stomp_device_normals.argtypes = [C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, dp]
+    _lib = l
+    return l
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _check(rc: int, handle=None):
+    if rc != 0:
+        l = load_library()
+        msg = (l.stomp_engine_last_error(handle) if handle else l.stomp_last_error()).decode()
+        raise RuntimeError(f"stomp engine error {rc}: {msg}")
+
+
+def sdf_build_device(problem, device_tensor_ptr: int, stream: int = 0):
+    """Builds problem.grid's distance field directly into a device buffer of n^3 floats."""
+    l = load_library()
+    g = problem.grid
+    boxes = np.array([list(b.center) + list(b.dims) for b in problem.boxes], np.float64).reshape(-1)
+    cyl = np.array([list(c.center) + [c.radius, c.length] for c in problem.cylinders], np.float64).reshape(-1)
+    origin = np.array(g.origin, np.float64)
+    boxes = boxes if boxes.size else np.zeros(1)
+    cyl = cyl if cyl.size else np.zeros(1)
+    _check(l.stomp_sdf_build(g.n, g.n, g.n, _dp(origin), g.resolution, g.max_expansion, _dp(boxes),
+                             len(problem.boxes), _dp(cyl), len(problem.cylinders), C.c_void_p(device_tensor_ptr),
+                             C.c_void_p(stream)))
+
+
+class Engine:
+    """One planning problem on one device: the StompOptimizer / PolicyImprovementLoop pair."""
+
+    def __init__(self, problem, device: int = 0, sdf_device_ptr: Optional[int] = None, stream: Optional[int] = None,
+                 rank: int = 0, world_size: int = 1, comm_id: Optional[bytes] = None):
+        l = load_library()
+        p = problem
+        self.problem = p
+        self.J, self.N, self.K = p.J, p.N, p.params.num_rollouts
+        self.S = len(p.spheres)
+        self._segs = (stomp_segment * len(p.robot.segments))(*[
+            stomp_segment(s.parent, s.q_index, (C.c_double * 9)(*s.rot), (C.c_double * 3)(*s.trans),
+                          (C.c_double * 3)(*s.axis)) for s in p.robot.segments])
+        self._sph = (stomp_sphere * max(self.S, 1))(*[
+            stomp_sphere(s.segment, s.radius, s.clearance, (C.c_double * 3)(*s.pos)) for s in p.spheres])
+        self._joints = (stomp_joint * self.J)(*[
+            stomp_joint(int(j.has_limits), j.min, j.max, j.joint_cost) for j in p.robot.joints])
+        pr = p.params
+        self._sig = np.full(self.J, pr.noise_stddev, np.float64)
+        self._dec = np.full(self.J, pr.noise_decay, np.float64)
+        self._start = np.ascontiguousarray(p.start, np.float64)
+        self._goal = np.ascontiguousarray(p.goal, np.float64)
+        g = p.grid
+        d = stomp_engine_desc()
+        d.abi_version = ABI_VERSION
+        d.num_joints, d.num_time_steps, d.num_rollouts = self.J, self.N, self.K
+        d.num_reused_rollouts = pr.num_reused_rollouts
+        d.num_segments = len(p.robot.segments)
+        d.segments = self._segs
+        d.num_spheres = self.S
+        d.spheres = self._sph
+        d.joints = self._joints
+        if sdf_device_ptr is not None:
+            grid_ptr, on_dev = sdf_device_ptr, 1
+        else:
+            self._sdf = np.ascontiguousarray(p.sdf, np.float32)
+            grid_ptr, on_dev = self._sdf.ctypes.data, 0
+        d.grid = stomp_grid(g.n, g.n, g.n, (C.c_double * 3)(*g.origin), g.resolution, C.c_void_p(grid_ptr), on_dev)
+        d.discretization = pr.trajectory_discretization
+        d.smoothness_costs = (C.c_double * 3)(pr.smoothness_cost_velocity, pr.smoothness_cost_acceleration,
+                                              pr.smoothness_cost_jerk)
+        d.ridge_factor = pr.ridge_factor
+        d.smoothness_cost_weight = pr.smoothness_cost_weight
+        d.obstacle_cost_weight = pr.obstacle_cost_weight
+        d.constraint_cost_weight = pr.constraint_cost_weight
+        d.torque_cost_weight = pr.torque_cost_weight
+        d.noise_stddev = _dp(self._sig)
+        d.noise_decay = _dp(self._dec)
+        d.use_cumulative_costs = int(pr.use_cumulative_costs)
+        d.start = _dp(self._start)
+        d.goal = _dp(self._goal)
+        d.seed = p.seed
+        d.max_iterations = pr.max_iterations
+        d.max_iterations_after_collision_free = pr.max_iterations_after_collision_free
+        d.device = device
+        d.stream = C.c_void_p(stream) if stream else None
+        d.rank = rank
+        d.world_size = world_size
+        self._comm = C.create_string_buffer(comm_id, 128) if comm_id else None
+        d.comm_id = C.cast(self._comm, C.c_void_p) if comm_id else None
+        self._desc = d
+        h = C.c_void_p()
+        _check(l.stomp_engine_create(C.byref(d), C.byref(h)))
+        self.h = h
+        first, count = C.c_int32(), C.c_int32()
+        l.stomp_engine_local_rollouts(self.h, C.byref(first), C.byref(count))
+        self.first, self.K_loc = first.value, count.value
+
+    def close(self):
+        h = getattr(self, "h", None)
+        if h:
+            load_library().stomp_engine_destroy(h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---------------------------------------------------------------- API
+    def theta(self) -> np.ndarray:
+        out = np.zeros((self.J, self.N))
+        _check(load_library().stomp_engine_get_theta(self.h, _dp(out)), self.h)
+        return out
+
+    def set_theta(self, theta):
+        t = np.ascontiguousarray(theta, np.float64)
+        _check(load_library().stomp_engine_set_theta(self.h, _dp(t)), self.h)
+
+    def iterate(self, iteration_number: int):
+        o = stomp_iter_out()
+        _check(load_library().stomp_engine_iterate(self.h, iteration_number, C.byref(o)), self.h)
+        return o.cost, bool(o.collision_free)
+
+    def run(self, first_iteration: int, count: int):
+        _check(load_library().stomp_engine_run(self.h, first_iteration, count), self.h)
+
+    def synchronize(self):
+        _check(load_library().stomp_engine_synchronize(self.h), self.h)
+
+    def execute(self, params, iteration_member: int = 1):
+        prm = np.ascontiguousarray(params, np.float64)
+        single = prm.ndim == 2
+        prm = prm.reshape(-1, self.J, self.N)
+        n = prm.shape[0]
+        costs = np.zeros((n, self.N))
+        cf = np.zeros(n, np.uint8)
+        traj = np.zeros((n, self.J, self.N))
+        _check(load_library().stomp_engine_eval(self.h, _dp(prm), n, _dp(costs), cf.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                _dp(traj), iteration_member), self.h)
+        if single:
+            return costs[0], bool(cf[0]), traj[0]
+        return costs, cf.astype(bool), traj
+
+    def optimize(self):
+        st = stomp_stats()
+        costs = np.zeros(max(self.problem.params.max_iterations, 1))
+        _check(load_library().stomp_engine_optimize(self.h, C.byref(st), _dp(costs)), self.h)
+        return st, costs[: st.iterations]
+
+    def best_trajectory(self) -> np.ndarray:
+        out = np.zeros((self.J, self.N))
+        _check(load_library().stomp_engine_get_best_trajectory(self.h, _dp(out)), self.h)
+        return out
+
+    def last_trajectory(self) -> np.ndarray:
+        out = np.zeros((self.J, self.N))
+        _check(load_library().stomp_engine_get_last_trajectory(self.h, _dp(out)), self.h)
+        return out
+
+    def rollouts(self, which: str) -> np.ndarray:
+        shape = (self.K_loc, self.N) if which == "state_costs" else (self.K_loc, self.J, self.N)
+        out = np.zeros(shape)
+        _check(load_library().stomp_engine_get_rollouts(self.h, which.encode(), _dp(out)), self.h)
+        return out
+
+    def matrix(self, which: str, joint: int = 0) -> np.ndarray:
+        out = np.zeros((self.N, self.N))
+        _check(load_library().stomp_engine_get_matrix(self.h, which.encode(), joint, _dp(out)), self.h)
+        return out
+
+    def pad_positions(self) -> np.ndarray:
+        out = np.zeros((12, self.S, 3))
+        _check(load_library().stomp_engine_get_pad_positions(self.h, _dp(out)), self.h)
+        return out
+
+    def set_timing(self, enable: bool):
+        _check(load_library().stomp_engine_set_timing(self.h, int(enable)), self.h)
+
+    def timing(self, name: str):
+        t, n = C.c_double(), C.c_int32()
+        _check(load_library().stomp_engine_get_timing(self.h, name.encode(), C.byref(t), C.byref(n)), self.h)
+        return t.value, n.value
+
+
+class DeviceBuffer:
+    """Engine-runtime device allocation (keeps torch's bundled HIP runtime out of the process)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        p = C.c_void_p()
+        _check(load_library().stomp_device_alloc(device, nbytes, C.byref(p)))
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def to_numpy(self, dtype, shape):
+        out = np.empty(shape, dtype)
+        assert out.nbytes <= self.nbytes
+        _check(load_library().stomp_device_copy_to_host(out.ctypes.data, C.c_void_p(self.ptr), out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            load_library().stomp_device_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    load_library().stomp_device_count(C.byref(n))
+    return n.value
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(load_library().stomp_comm_unique_id(buf))
+    return buf.raw
+
+
+def device_math(x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float64)
+    n = len(x)
+    outs = [np.zeros(n) for _ in range(5)]
+    _check(load_library().stomp_device_selftest(_dp(x), n, *[_dp(o) for o in outs]))
+    return outs
+
+
+def device_normals(seed: int, iteration: int, joint: int, rollout: int, n: int) -> np.ndarray:
+    z = np.zeros(n)
+    _check(load_library().stomp_device_normals(seed, iteration, joint, rollout, n, _dp(z)))
+    return z
