@@ -248,14 +248,16 @@ static void fk_spheres(const so_problem* P, const double* q, frame_t* frames, do
 
 /* ---------------------------------------------------------------- distance field
  * distance_field::PropagationDistanceField::getDistanceGradient (3rd party; call site
- * stomp_collision_space.h:187-191): nearest cell = round((p - origin) / res); cells
- * with an index < 1 or >= n-1 (or a non-finite position) read distance 0. */
+ * stomp_collision_space.h:187-191): nearest cell = round((p - origin) * (1/res)) (VoxelGrid
+ * keeps the reciprocal resolution); cells with an index < 1 or >= n-1 (or a non-finite
+ * position) read distance 0. */
 double so_sdf_distance(const so_problem* P, double x, double y, double z)
 {
     const so_sdf* g = &P->cfg.sdf;
-    double fx = round((x - g->origin[0]) / g->resolution);
-    double fy = round((y - g->origin[1]) / g->resolution);
-    double fz = round((z - g->origin[2]) / g->resolution);
+    const double inv = 1.0 / g->resolution;
+    double fx = round((x - g->origin[0]) * inv);
+    double fy = round((y - g->origin[1]) * inv);
+    double fz = round((z - g->origin[2]) * inv);
     if (!(fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(g->nx - 1) && fy < (double)(g->ny - 1) &&
           fz < (double)(g->nz - 1)))
         return 0.0;

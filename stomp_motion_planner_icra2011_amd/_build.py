@@ -17,8 +17,8 @@ LIB = os.path.join(PKG, "libstomp_engine.so")
 BUILD = os.path.join(ROOT, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["kernels.hip", "selftest.hip", "engine.cpp", "setup.cpp"]
-HEADERS = ["kernels.h", "setup.h", "stomp_math.h"]
+SOURCES = ["k_noise.hip", "k_cost.hip", "k_weights.hip", "k_misc.hip", "selftest.hip", "engine.cpp", "setup.cpp"]
+HEADERS = ["kernels.h", "setup.h", "stomp_math.h", "device_fk.h"]
 
 # One rounding per operation on host and device (parity with the oracle's FP contract).
 COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-Wall",
@@ -33,32 +33,36 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> str:
+def build(verbose: bool = False, force: bool = False, jobs: int = 4, variant: str = "") -> str:
+    """variant "stamps": diagnostic library with in-kernel phase stamps (libstomp_engine_stamps.so)."""
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "stomp_engine.h")]
+    extra = ["-DSTOMP_STAMPS"] if variant == "stamps" else []
+    lib = LIB.replace(".so", "_" + variant + ".so") if variant else LIB
+    suffix = ("." + variant) if variant else ""
     objs, procs = [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(BUILD, src + ".o")
+        obj = os.path.join(BUILD, src + suffix + ".o")
         objs.append(obj)
         if not force and not _newer(obj, [path] + hdrs):
             continue
-        cmd = [HIPCC] + COMMON + ARCH + ["-x", "hip", "-c", path, "-o", obj]
+        cmd = [HIPCC] + COMMON + extra + ARCH + ["-x", "hip", "-c", path, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         if len(procs) >= jobs:
             _wait(procs)
     _wait(procs)
-    if force or _newer(LIB, objs):
-        cmd = [HIPCC] + ARCH + ["-shared", "-fPIC", "-o", LIB] + objs + ["-L/opt/rocm/lib", "-lrccl",
+    if force or _newer(lib, objs):
+        cmd = [HIPCC] + ARCH + ["-shared", "-fPIC", "-o", lib] + objs + ["-L/opt/rocm/lib", "-lrccl",
                                                                          "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout)
-    return LIB
+    return lib
 
 
 def _wait(procs):
@@ -73,4 +77,4 @@ def _wait(procs):
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    print(build(verbose=True, force="--force" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))

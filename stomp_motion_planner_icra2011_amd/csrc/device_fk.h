@@ -1,0 +1,136 @@
+// device_fk.h -- device-side kinematics, distance-field lookup and potential.
+//
+// KDL conventions restated (orocos KDL is third party, reached from
+// treefksolverjointposaxis_partial.cpp:125,168 and stomp_collision_point.h:138-141):
+// Rotation::Rot2, Rotation*Rotation, Frame*Frame and Frame*Vector, each sum
+// evaluated left to right with one rounding per operation.
+#pragma once
+
+#include "kernels.h"
+#include "stomp_math.h"
+
+namespace stomp {
+
+struct Frame {
+    double R[9];
+    double p[3];
+};
+
+__device__ __forceinline__ void rotmul(const double* A, const double* B, double* C)
+{
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = A[3 * i + 0] * B[0 + j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// out = parent * Frame(rot, trans) * Frame(Rot2(axis, q), 0), with (st, ct) = (sin q, cos q)
+// precomputed; parent == nullptr is the identity (root segment).  out must not alias parent.
+__device__ __forceinline__ void compose(const DevSegment& sg, const Frame* parent, double st, double ct, Frame& out)
+{
+    Frame pose;
+    if (sg.q_index >= 0) {
+        const double* a = sg.axis;
+        const double vt = 1.0 - ct;
+        const double m_vt_0 = vt * a[0], m_vt_1 = vt * a[1], m_vt_2 = vt * a[2];
+        const double m_st_0 = a[0] * st, m_st_1 = a[1] * st, m_st_2 = a[2] * st;
+        const double m_vt_0_1 = m_vt_0 * a[1], m_vt_0_2 = m_vt_0 * a[2], m_vt_1_2 = m_vt_1 * a[2];
+        double Rq[9];
+        Rq[0] = ct + m_vt_0 * a[0];
+        Rq[1] = -m_st_2 + m_vt_0_1;
+        Rq[2] = m_st_1 + m_vt_0_2;
+        Rq[3] = m_st_2 + m_vt_0_1;
+        Rq[4] = ct + m_vt_1 * a[1];
+        Rq[5] = -m_st_0 + m_vt_1_2;
+        Rq[6] = -m_st_1 + m_vt_0_2;
+        Rq[7] = m_st_0 + m_vt_1_2;
+        Rq[8] = ct + m_vt_2 * a[2];
+        rotmul(sg.rot, Rq, pose.R);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) pose.R[k] = sg.rot[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pose.p[k] = sg.trans[k];
+    if (!parent) {
+        out = pose;
+        return;
+    }
+    rotmul(parent->R, pose.R, out.R);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        out.p[i] = parent->R[3 * i + 0] * pose.p[0] + parent->R[3 * i + 1] * pose.p[1] +
+                   parent->R[3 * i + 2] * pose.p[2] + parent->p[i];
+}
+
+__device__ __forceinline__ void apply(const double* R, const double* P, const double* v, double* o)
+{
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[i] = R[3 * i + 0] * v[0] + R[3 * i + 1] * v[1] + R[3 * i + 2] * v[2] + P[i];
+}
+
+// One FK program step (see FkOp).  Saved-frame moves are per-element selects under a
+// wave-uniform branch: branchy assignment lets the optimiser sink the stores through a
+// pointer select and send the frames to scratch.
+__device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, double st, double ct, Frame& C,
+                                      Frame& S0, Frame& S1)
+{
+    Frame nf;
+    if (base == kBaseChain) {
+        compose(sg, &C, st, ct, nf);
+    } else if (base == kBaseRoot) {
+        compose(sg, nullptr, st, ct, nf);
+    } else {
+        Frame P;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P.R[k] = base == 0 ? S0.R[k] : S1.R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) P.p[k] = base == 0 ? S0.p[k] : S1.p[k];
+        compose(sg, &P, st, ct, nf);
+    }
+    C = nf;
+    if (save >= 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            S0.R[k] = save == 0 ? C.R[k] : S0.R[k];
+            S1.R[k] = save == 1 ? C.R[k] : S1.R[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            S0.p[k] = save == 0 ? C.p[k] : S0.p[k];
+            S1.p[k] = save == 1 ? C.p[k] : S1.p[k];
+        }
+    }
+}
+
+// distance_field::getDistanceGradient cell rule (3rd party; call site stomp_collision_space.h:190):
+// nearest cell round((p - origin) * (1/res)); cells with an index < 1 or >= n-1 read 0.
+// Branch-free so a lane's gathers can all be in flight together: an out-of-range lane
+// loads cell 0 and discards it.
+__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
+{
+    const double fx = round((p[0] - m.ox) * m.inv_res);
+    const double fy = round((p[1] - m.oy) * m.inv_res);
+    const double fz = round((p[2] - m.oz) * m.inv_res);
+    const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
+                    fz < (double)(m.nz - 1);
+    const size_t idx = ok ? ((size_t)(int)fx * m.ny + (size_t)(int)fy) * m.nz + (size_t)(int)fz : 0;
+    const float v = m.sdf[idx];
+    return ok ? v : 0.0f;
+}
+
+// StompCollisionSpace::getCollisionPointPotentialGradient (stomp_collision_space.h:193-228)
+__device__ __forceinline__ double potential(const DevSphere& s, double dist)
+{
+    const double d = dist - s.radius;
+    if (d >= s.clearance) return 0.0;
+    if (d >= 0.0) {
+        const double diff = d - s.clearance;
+        const double gm = diff * s.inv_clearance;
+        return 0.5 * gm * diff;
+    }
+    return -d + 0.5 * s.clearance;
+}
+
+}  // namespace stomp

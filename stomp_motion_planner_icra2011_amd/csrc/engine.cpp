@@ -50,6 +50,10 @@ struct stomp_engine {
     SetupOutput su;
     DevModel model{};
     std::vector<FkOp> ops;
+    std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
+    int nslots = 0;
+    double* d_frames = nullptr;     // [frames_cap][nslots][12][N]
+    int frames_cap = 0;
     std::vector<void*> allocs;
     double *d_theta = nullptr, *d_LT = nullptr, *d_MT = nullptr, *d_QT = nullptr;
     double *d_params = nullptr, *d_noise = nullptr, *d_control = nullptr, *d_prob = nullptr, *d_state = nullptr;
@@ -63,6 +67,8 @@ struct stomp_engine {
     int* d_pad_cf = nullptr;
     int pad_collision = 0;
     bool reused_next = false, extra_added = false;
+    int pending_member = -1;   // iteration_ of a noiseless rollout of theta not evaluated yet
+    double *d_mm = nullptr, *d_psum_part = nullptr, *d_psum_all = nullptr, *d_u_part = nullptr, *d_u_all = nullptr;
     int K_gen = 0;
     double* h_total = nullptr;
     uint8_t* h_cf = nullptr;
@@ -192,44 +198,50 @@ int plan_fk(stomp_engine* e, const stomp_engine_desc* d, std::vector<FkOp>& ops)
         prev = s;
         for (int a = s; a >= 0 && !needed[a]; a = d->segments[a].parent) needed[a] = 1;
     }
+    // DFS order: the next needed segment after s is its first needed child, so a chain
+    // continues from the running frame C; a segment with several needed children is saved
+    // and its later children start from the saved copy.
     std::vector<int> remaining(ns, 0), slot_of(ns, -1);
     for (int s = 0; s < ns; ++s)
         if (needed[s] && d->segments[s].parent >= 0) remaining[d->segments[s].parent]++;
-    bool used[kSlots] = {false, false, false, false};
-    auto alloc = [&]() {
-        for (int k = 0; k < kSlots; ++k)
-            if (!used[k]) { used[k] = true; return k; }
-        return -1;
-    };
-    int sph = 0;
+    bool used[kSaves] = {false, false};
+    const int runmax = run_max(d->num_time_steps);
+    int sph = 0, cur = -1;
     for (int s = 0; s < ns; ++s) {
         if (!needed[s]) continue;
         const int p = d->segments[s].parent;
-        int from = p >= 0 ? slot_of[p] : -1, to;
-        if (p >= 0 && --remaining[p] == 0) {
-            to = from;   // parent frame dead after this child: overwrite in place
+        int base;
+        if (p < 0) base = kBaseRoot;
+        else if (p == cur) base = kBaseChain;
+        else if (slot_of[p] >= 0) base = slot_of[p];
+        else return fail(e, STOMP_E_UNSUPPORTED, "FK planner: parent frame of segment %d not available", s);
+        if (p >= 0 && --remaining[p] == 0 && slot_of[p] >= 0) {
+            used[slot_of[p]] = false;   // read by this step before any save below overwrites it
             slot_of[p] = -1;
-        } else {
-            to = alloc();
-            if (to < 0) return fail(e, STOMP_E_UNSUPPORTED, "kinematic tree needs more than %d live frames", kSlots);
         }
-        slot_of[s] = to;
+        int save = -1;
+        if (remaining[s] >= 2) {
+            for (int k = 0; k < kSaves; ++k)
+                if (!used[k]) { used[k] = true; save = k; break; }
+            if (save < 0) return fail(e, STOMP_E_UNSUPPORTED, "kinematic tree needs more than %d saved frames", kSaves);
+            slot_of[s] = save;
+        }
+        cur = s;
         int b = sph;
         while (sph < d->num_spheres && d->spheres[sph].segment == s) ++sph;
+        const int slot = sph > b ? e->nslots++ : -1;
+        for (int j = b; j < sph; ++j) e->sphere_slot[j] = slot;
         bool first = true;
-        for (int a = b; a < sph || first; a += kRunMax) {
+        for (int a = b; a < sph || first; a += runmax) {
             FkOp o;
             o.seg = first ? s : -1;
-            o.from = first ? from : to;
-            o.to = to;
+            o.base = first ? base : kBaseChain;
+            o.save = first ? save : -1;
+            o.slot = first ? slot : -1;
             o.sph_begin = std::min(a, sph);
-            o.sph_end = std::min(a + kRunMax, sph);
+            o.sph_end = std::min(a + runmax, sph);
             ops.push_back(o);
             first = false;
-        }
-        if (remaining[s] == 0) {
-            used[to] = false;
-            slot_of[s] = -1;
         }
     }
     return 0;
@@ -250,7 +262,39 @@ void release(stomp_engine* e)
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
 }
 
-int enqueue_iteration(stomp_engine* e, int it)
+// noiseless rollout of the current theta (policy_improvement_loop.cpp:180-182), alone
+void launch_noiseless(stomp_engine* e, int member)
+{
+    Timed tm(e, T_NOISELESS);
+    CostArgs ca{};
+    ca.frames = e->d_frames;
+    ca.num_noisy = 0;
+    ca.x_params = e->d_theta; ca.x_member = member;
+    ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+    launch_cost(e->model, ca, e->stream);
+}
+
+int flush_noiseless(stomp_engine* e)
+{
+    if (e->pending_member >= 0) {
+        launch_noiseless(e, e->pending_member);
+        e->pending_member = -1;
+    }
+    return 0;
+}
+
+#ifdef STOMP_WITH_RCCL
+#define NCCL_TRY(e, x)                                                                       \
+    do {                                                                                     \
+        ncclResult_t _r = (x);                                                               \
+        if (_r != ncclSuccess) return fail((e), STOMP_E_COMM, "%s: %s", #x, ncclGetErrorString(_r)); \
+    } while (0)
+#endif
+
+// One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
+// pipelined: the noiseless rollout of the updated theta is not launched here but evaluated by
+// the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
+int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
 {
     const int member = it - 1;
     NoiseArgs na{};
@@ -261,7 +305,8 @@ int enqueue_iteration(stomp_engine* e, int it)
     std::memcpy(na.dcoef, e->su.dcoef, sizeof na.dcoef);
     const double w = 0.5 * e->w_smooth;   // policy_improvement.cpp:487
     for (int r = 0; r < 3; ++r) na.wr[r] = w * e->smooth[r];
-    na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0;
+    na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0; na.row_begin = 0;
+    if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
 
     // generateRollouts bookkeeping (policy_improvement.cpp:167-175)
     e->K_gen = e->K - e->Kr;
@@ -269,6 +314,7 @@ int enqueue_iteration(stomp_engine* e, int it)
         e->K_gen = e->K;
         if (e->Kr > 0) e->reused_next = true;
     } else {
+        flush_noiseless(e);
         Timed tm(e, T_REUSE);
         launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, e->extra_added ? 1 : 0, e->d_params, e->d_noise, e->d_state,
                      e->d_control, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params,
@@ -278,43 +324,69 @@ int enqueue_iteration(stomp_engine* e, int it)
     na.K_gen_global = e->K_gen;
     {
         Timed tm(e, T_NOISE);
-        launch_noise(na, 4, e->stream);
+        launch_noise(na, e->stream);
     }
-    // Task::execute for the generated rollouts of this shard
-    int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
-    if (g1 > g0) {
+    // Task::execute for the generated rollouts of this shard (+ the pending noiseless rollout)
+    {
+        const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
+        CostArgs ca{};
+        ca.frames = e->d_frames;
+        ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = std::max(g1 - g0, 0);
+        ca.member = member; ca.state_out = e->d_state;
+        if (e->pending_member >= 0) {
+            ca.x_params = e->d_theta; ca.x_member = e->pending_member;
+            ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+            e->pending_member = -1;
+        }
         Timed tm(e, T_COST);
-        launch_rollout_cost(e->model, e->d_params, (long long)e->J * e->N, g1 - g0, e->d_state, nullptr, nullptr,
-                            nullptr, member, e->stream);
+        launch_cost(e->model, ca, e->stream);
     }
     WeightArgs wa{};
     wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
     wa.state = e->d_state; wa.control = e->d_control; wa.noise = e->d_noise;
-    wa.cum = nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
+    wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
+    wa.tc = weights_tile(e->K_loc);
+    wa.nb_total = e->K / kSumBlock;
+    wa.mm = e->d_mm; wa.psum_part = e->d_psum_part; wa.psum_all = e->d_psum_all; wa.u_part = e->d_u_part;
     {
         Timed tm(e, T_WEIGHTS);
-        if (e->use_cum) {
-            wa.cum = e->d_cum;
-            launch_cumulative(wa, e->stream);
+        if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
+        if (e->world == 1) {
+            wa.mode = W_FUSED;
+            launch_weights(wa, e->stream);
+        } else {
+#ifdef STOMP_WITH_RCCL
+            const size_t JN = (size_t)e->J * e->N;
+            const size_t nb_loc = (size_t)e->K_loc / kSumBlock;
+            wa.mode = W_MINMAX;
+            launch_weights(wa, e->stream);
+            NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
+            wa.mode = W_PSUM;
+            launch_weights(wa, e->stream);
+            NCCL_TRY(e, ncclAllGather(e->d_psum_part, e->d_psum_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
+            wa.mode = W_USUM;
+            launch_weights(wa, e->stream);
+            NCCL_TRY(e, ncclAllGather(e->d_u_part, e->d_u_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
+#endif
         }
-        launch_weights(wa, e->stream);
     }
     {
         Timed tm(e, T_UPDATE);
-        launch_update(e->J, e->N, e->d_MT, e->d_u, e->d_theta, e->stream);
+        launch_update(e->J, e->N, e->d_MT, e->d_u, e->world > 1 ? e->d_u_all : nullptr, e->K / kSumBlock,
+                      e->d_theta, e->stream);
     }
-    {
-        Timed tm(e, T_NOISELESS);
-        launch_rollout_cost(e->model, e->d_theta, 0, 1, e->d_x_state, e->d_cf, e->d_last_traj, e->d_total, member,
-                            e->stream);
+    if (pipelined) {
+        e->pending_member = member;
+    } else {
+        launch_noiseless(e, member);
     }
     if (e->Kr > 0) {
         // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0
         hipMemcpyAsync(e->d_x_params, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToDevice, e->stream);
         NoiseArgs xa = na;
-        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 1;
+        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 1; xa.row_begin = 0;
         xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
-        launch_noise(xa, 1, e->stream);
+        launch_noise(xa, e->stream);
         e->extra_added = true;
     }
     hipError_t st = hipGetLastError();
@@ -410,6 +482,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         }                                       \
     } while (0)
 
+    e->sphere_slot.assign(std::max(e->S, 1), 0);
     CREATE_TRY(plan_fk(e, d, e->ops));
     SetupInput si;
     si.J = e->J; si.N = e->N; si.discretization = e->disc;
@@ -442,7 +515,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     std::vector<DevSphere> sph(std::max(e->S, 1));
     for (int j = 0; j < e->S; ++j) {
         const stomp_sphere& g = d->spheres[j];
-        sph[j].segment = g.segment; sph[j].pad_ = 0;
+        sph[j].segment = g.segment; sph[j].slot = e->sphere_slot[j];
         sph[j].radius = g.radius; sph[j].clearance = g.clearance;
         sph[j].inv_clearance = 1.0 / g.clearance;   // stomp_collision_point.cpp:50
         std::memcpy(sph[j].pos, g.pos, sizeof g.pos);
@@ -454,7 +527,11 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         jmin[j] = d->joints[j].min;
         jmax[j] = d->joints[j].max;
     }
-    DevSegment* d_segs; DevSphere* d_sph; FkOp* d_ops; int* d_hl; double *d_jmin, *d_jmax;
+    // slots are numbered in sphere order, so each slot owns a contiguous sphere range
+    std::vector<int> slot_sph(e->nslots + 1, e->S);
+    for (int j = e->S - 1; j >= 0; --j) slot_sph[e->sphere_slot[j]] = j;
+    DevSegment* d_segs; DevSphere* d_sph; FkOp* d_ops; int* d_hl; int* d_slot_sph; double *d_jmin, *d_jmax;
+    CREATE_TRY(upload(e, &d_slot_sph, slot_sph.data(), slot_sph.size()));
     CREATE_TRY(upload(e, &d_segs, segs.data(), segs.size()));
     CREATE_TRY(upload(e, &d_sph, sph.data(), sph.size()));
     CREATE_TRY(upload(e, &d_ops, e->ops.data(), e->ops.size()));
@@ -481,6 +558,16 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
     if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
+    e->frames_cap = e->K_loc + 1;
+    CREATE_TRY(dev_alloc(e, &e->d_frames, (size_t)e->frames_cap * std::max(e->nslots, 1) * 12 * N));
+    if (world > 1) {
+        const size_t nb_loc = (size_t)e->K_loc / kSumBlock, nb_tot = (size_t)e->K / kSumBlock;
+        CREATE_TRY(dev_alloc(e, &e->d_mm, 2 * (size_t)J * N));
+        CREATE_TRY(dev_alloc(e, &e->d_psum_part, nb_loc * J * N));
+        CREATE_TRY(dev_alloc(e, &e->d_psum_all, nb_tot * J * N));
+        CREATE_TRY(dev_alloc(e, &e->d_u_part, nb_loc * J * N));
+        CREATE_TRY(dev_alloc(e, &e->d_u_all, nb_tot * J * N));
+    }
     CREATE_TRY(dev_alloc(e, &e->d_x_params, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_noise, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_control, (size_t)J * N));
@@ -498,13 +585,26 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
 
     DevModel& m = e->model;
-    m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size();
-    m.segs = d_segs; m.sph = d_sph; m.ops = d_ops; m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
+    m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size(); m.nseg = e->nseg;
+    m.nslots = e->nslots;
+    m.sph_chunk = pairs_sphere_chunk(std::max(e->S, 1), N);
+    for (int g = 0; g < e->nslots; ++g) m.sph_chunk = std::max(m.sph_chunk, slot_sph[g + 1] - slot_sph[g]);
+    if ((size_t)m.sph_chunk * N * sizeof(double) + (size_t)e->S * sizeof(DevSphere) > 64 * 1024)
+        CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "%d spheres on one segment x %d waypoints exceed the LDS budget",
+                        m.sph_chunk, N));
+    if (!cost_supported(m)) CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "FK program too large (%d ops, %d segments)",
+                                            m.nops, m.nseg));
+    m.segs = d_segs; m.sph = d_sph; m.ops = d_ops; m.slot_sph = d_slot_sph; m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
+    m.inv_res = 1.0 / d->grid.resolution;
     m.start = e->d_start; m.goal = e->d_goal;
     const double invTime = 1.0 / e->disc;   // stomp_optimizer.cpp:620
-    for (int k = 0; k < 7; ++k) m.vel_coef[k] = invTime * kDiffRules[0][k];
+    for (int k = 0; k < 7; ++k) {
+        m.vel_coef[k] = invTime * kDiffRules[0][k];
+        if ((k < kVelTap0 || k > kVelTap1) && kDiffRules[0][k] != 0.0)
+            CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "velocity rule tap %d outside the kernel's stencil", k));
+    }
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
     m.has_limits = d_hl; m.jmin = d_jmin; m.jmax = d_jmax; m.QT = e->d_QT;
     m.pad_collision = 0;
@@ -554,7 +654,8 @@ int stomp_engine_set_theta(stomp_engine* e, const double* theta)
 
 int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
 {
-    int rc = enqueue_iteration(e, it);
+    flush_noiseless(e);
+    int rc = enqueue_iteration(e, it, false);
     if (rc) return rc;
     HIP_TRY(e, hipMemcpyAsync(e->h_total, e->d_total, sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(e->h_cf, e->d_cf, 1, hipMemcpyDeviceToHost, e->stream));
@@ -569,9 +670,10 @@ int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
 int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count)
 {
     for (int i = 0; i < count; ++i) {
-        int rc = enqueue_iteration(e, first_iteration + i);
+        int rc = enqueue_iteration(e, first_iteration + i, true);
         if (rc) return rc;
     }
+    flush_noiseless(e);
     return 0;
 }
 
@@ -599,9 +701,20 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
         if ((rc = dev_alloc(e, &e->d_eval_cf, (size_t)num))) return rc;
         e->eval_cap = num;
     }
+    if (num > e->frames_cap) {
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        hipFree(e->d_frames);
+        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->d_frames), e->allocs.end());
+        int rc;
+        if ((rc = dev_alloc(e, &e->d_frames, (size_t)num * std::max(e->nslots, 1) * 12 * e->N))) return rc;
+        e->frames_cap = num;
+    }
     HIP_TRY(e, hipMemcpyAsync(e->d_eval_params, params, sizeof(double) * num * JN, hipMemcpyHostToDevice, e->stream));
-    launch_rollout_cost(e->model, e->d_eval_params, (long long)JN, num, e->d_eval_costs, e->d_eval_cf,
-                        traj_out ? e->d_eval_traj : nullptr, nullptr, iteration_member, e->stream);
+    CostArgs ca{};
+    ca.frames = e->d_frames;
+    ca.params = e->d_eval_params; ca.stride = (long long)JN; ca.num_noisy = num; ca.member = iteration_member;
+    ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf; ca.traj_out = traj_out ? e->d_eval_traj : nullptr;
+    launch_cost(e->model, ca, e->stream);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipMemcpyAsync(costs, e->d_eval_costs, sizeof(double) * num * e->N, hipMemcpyDeviceToHost, e->stream));
     if (collision_free)

@@ -1,0 +1,158 @@
+// k_misc.hip -- setup-time and bookkeeping kernels: padding-point FK, rollout reuse,
+// distance-field construction.
+#include "device_fk.h"
+
+namespace stomp {
+
+// padding-point sphere positions: iteration-0 full FK of start (rows 0..5) and goal (rows 6..11)
+// (stomp_optimizer.cpp:626-630 with JntToCartFull; padding rows of the group trajectory hold
+// start/goal, stomp_trajectory.cpp:94-107)
+__global__ void k_pad_fk(DevModel m, const double* start, const double* goal, double* pad_pos, int* pad_cf)
+{
+    const int side = threadIdx.x;
+    if (side > 1) return;
+    const double* q = side ? goal : start;
+    Frame C, S0, S1;
+    bool col = false;
+    for (int op = 0; op < m.nops; ++op) {
+        const FkOp o = m.ops[op];
+        if (o.seg >= 0) {
+            const DevSegment& sg = m.segs[o.seg];
+            double st = 0.0, ct = 1.0;
+            if (sg.q_index >= 0) det_sincos(q[sg.q_index], &st, &ct);
+            fk_op(sg, o.base, o.save, st, ct, C, S0, S1);
+        }
+        for (int s = o.sph_begin; s < o.sph_end; ++s) {
+            double p[3];
+            apply(C.R, C.p, m.sph[s].pos, p);
+            if ((double)sdf_distance(m, p) <= m.sph[s].radius) col = true;
+            for (int row = 0; row < 6; ++row)
+                for (int c = 0; c < 3; ++c) pad_pos[((size_t)(side * 6 + row) * m.S + s) * 3 + c] = p[c];
+        }
+    }
+    if (col) atomicOr(pad_cf, 1);
+}
+
+void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
+                   hipStream_t s)
+{
+    hipLaunchKernelGGL(k_pad_fk, dim3(1), dim3(64), 0, s, m, start, goal, pad_pos, pad_cf);
+}
+
+// ============================================================== rollout reuse
+// PolicyImprovement::generateRollouts reuse branch (policy_improvement.cpp:176-225): rank the
+// K previous rollouts and the extra (noiseless) rollout by Rollout::getCost (:149-156),
+// lexicographic on (cost, index) with the extra rollout at index -1 (std::sort of pairs), copy
+// the best K_r into rows K_gen.. and re-base their noise on the current theta.
+__global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params,
+                                               double* noise, double* state, const double* control,
+                                               const double* x_params, const double* x_state,
+                                               const double* x_control, const double* theta, double* tmp_params,
+                                               double* tmp_state)
+{
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    const int n = K + with_extra;
+    double* costs = sh;
+    int* sel = (int*)(sh + n);
+    const int tid = threadIdx.x, bs = blockDim.x;
+    const size_t JN = (size_t)J * N;
+    for (int c = tid; c < n; c += bs) {
+        const double* st = c < K ? state + (size_t)c * N : x_state;
+        const double* ct = c < K ? control + (size_t)c * JN : x_control;
+        double s = st[0];
+        for (int t = 1; t < N; ++t) s += st[t];
+        for (int d = 0; d < J; ++d) {
+            double x = ct[(size_t)d * N];
+            for (int t = 1; t < N; ++t) x += ct[(size_t)d * N + t];
+            s += x;
+        }
+        costs[c] = s;
+    }
+    __syncthreads();
+    for (int c = tid; c < n; c += bs) {
+        const int ic = c < K ? c : -1;
+        const double cc = costs[c];
+        int rank = 0;
+        for (int c2 = 0; c2 < n; ++c2) {
+            const int ic2 = c2 < K ? c2 : -1;
+            const double x = costs[c2];
+            if (x < cc || (x == cc && ic2 < ic)) ++rank;
+        }
+        if (rank < Kr) sel[rank] = c;
+    }
+    __syncthreads();
+    for (size_t idx = tid; idx < (size_t)Kr * JN; idx += bs) {
+        const int r = (int)(idx / JN);
+        const size_t off = idx % JN;
+        const int src = sel[r];
+        tmp_params[idx] = src < K ? params[(size_t)src * JN + off] : x_params[off];
+    }
+    for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
+        const int r = (int)(idx / N);
+        const int t = (int)(idx % N);
+        const int src = sel[r];
+        tmp_state[idx] = src < K ? state[(size_t)src * N + t] : x_state[t];
+    }
+    __syncthreads();
+    for (size_t idx = tid; idx < (size_t)Kr * JN; idx += bs) {
+        const int r = (int)(idx / JN);
+        const size_t off = idx % JN;
+        const size_t dst = (size_t)(K_gen + r) * JN + off;
+        const double p = tmp_params[idx];
+        params[dst] = p;
+        noise[dst] = p - theta[off];
+    }
+    for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
+        const int r = (int)(idx / N);
+        const int t = (int)(idx % N);
+        state[(size_t)(K_gen + r) * N + t] = tmp_state[idx];
+    }
+}
+
+void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,
+                  double* state, const double* control, const double* x_params, const double* x_state,
+                  const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
+                  hipStream_t s)
+{
+    const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
+    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, params, noise, state,
+                       control, x_params, x_state, x_control, theta, tmp_params, tmp_state);
+}
+
+// ============================================================== distance field construction
+__global__ void k_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes, int nb,
+                            const long long* cyl_d2, const int* cyl_z, int nc, float* out)
+{
+    const long long total = (long long)nx * ny * nz;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int z = (int)(idx % nz);
+        const int y = (int)((idx / nz) % ny);
+        const int x = (int)(idx / ((long long)nz * ny));
+        long long d2 = cap2;
+        for (int b = 0; b < nb; ++b) {
+            const int* r = boxes + 6 * b;
+            long long dx = max(max(r[0] - x, 0), x - r[1]);
+            long long dy = max(max(r[2] - y, 0), y - r[3]);
+            long long dz = max(max(r[4] - z, 0), z - r[5]);
+            long long v = dx * dx + dy * dy + dz * dz;
+            if (v < d2) d2 = v;
+        }
+        for (int c = 0; c < nc; ++c) {
+            const long long dxy = cyl_d2[((size_t)c * nx + x) * ny + y];
+            long long dz = max(max(cyl_z[2 * c] - z, 0), z - cyl_z[2 * c + 1]);
+            long long v = dxy + dz * dz;
+            if (v < d2) d2 = v;
+        }
+        out[idx] = (float)(sqrt((double)d2) * res);
+    }
+}
+
+void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes, int nb, const long long* cyl_d2,
+                      const int* cyl_z, int nc, float* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_sdf_build, dim3(2048), dim3(256), 0, s, nx, ny, nz, cap2, res, boxes, nb, cyl_d2, cyl_z, nc,
+                       out);
+}
+
+}  // namespace stomp

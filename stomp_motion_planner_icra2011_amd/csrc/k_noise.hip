@@ -1,0 +1,208 @@
+// k_noise.hip -- noise sampling, projection and control cost, fused per (rollout tile, joint).
+//
+//   eps = sigma_d * (0 + L z)          MultivariateGaussian::sample (multivariate_gaussian.h:88-94)
+//                                      via generateRollouts (policy_improvement.cpp:228-236)
+//   params = theta + eps               policy_improvement.cpp:234
+//   nproj = M eps                      computeProjectedNoise (policy_improvement.cpp:473-482)
+//   control = sum_i w_i (D_i x)^2      computeControlCosts (covariant_trajectory_policy.cpp:228-255),
+//                                      x = padded (params + nproj), 7-tap stencils instead of dense D_i
+//
+// One workgroup owns RT rollouts of one joint; lane i owns time step i and keeps RT
+// accumulators.  L^T / M^T are read straight from L2 (lane i reads column i, so a wave's
+// load is 512 contiguous bytes) eight k at a time so eight loads are in flight per lane;
+// z and eps sit in LDS as [k][RT] so one k costs RT/2 broadcast ds_read_b128.  Sums run
+// over k in ascending order, one rounding per operation (the oracle's contract); the
+// triangular product stops at k = i exactly like the oracle's loop.
+#include "kernels.h"
+#include "stomp_math.h"
+#include "stamps.h"
+
+namespace stomp {
+
+// acc[rr] += sum_{k < kend} AT[k][i] * v[k][rr], k ascending.  Unconditional clamped loads,
+// double-buffered: the next eight AT values are in flight while the current eight are used.
+template <int RT>
+__device__ __forceinline__ void band_product(const double* __restrict__ AT, int N, int i, int kend,
+                                             const double* v, double* acc)
+{
+    double cur[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cur[q] = AT[(size_t)min(q, N - 1) * N + i];
+    for (int k0 = 0; k0 < kend; k0 += 8) {
+        double nxt[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nxt[q] = AT[(size_t)min(k0 + 8 + q, N - 1) * N + i];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double c = k0 + q < N ? cur[q] : 0.0;
+            const double* x = v + min(k0 + q, N - 1) * RT;
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr) acc[rr] += c * x[rr];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+}
+
+template <int BLOCK, int RT>
+__global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = a.N, Nall = a.Nall, J = a.J;
+    double* zs = lds;              // N*RT   [k][rr]
+    double* eps = zs + RT * N;     // N*RT   [k][rr]
+    double* xs = eps + RT * N;     // RT*Nall
+    double* cs = xs + RT * Nall;   // RT*Nall
+    const int d = blockIdx.y;
+    const int r0 = a.row_begin + blockIdx.x * RT;
+    const int tid = threadIdx.x;
+    const int i = tid;
+    const double sig = a.sigma.v[d];
+    STAMP(0);
+
+    bool gen[RT];
+    bool any_gen = false;
+#pragma unroll
+    for (int rr = 0; rr < RT; ++rr) {
+        const int r = r0 + rr;
+        const int g = a.first_global + r;
+        gen[rr] = (r < a.K_loc) && !a.zero_noise && g < a.K_gen_global;
+        any_gen |= gen[rr];
+    }
+    // standard normals of all generated rows, (row, pair) items spread over the whole block
+    {
+        const int P = (N + 1) / 2;
+        for (int idx = tid; idx < RT * P; idx += BLOCK) {
+            const int rr = idx / P, p = idx - rr * P;
+            const int r = r0 + rr, g = a.first_global + r;
+            if (!((r < a.K_loc) && !a.zero_noise && g < a.K_gen_global)) continue;
+            double z0, z1;
+            normal_pair(a.seed, a.iteration, d, g, p, &z0, &z1);
+            zs[(2 * p) * RT + rr] = z0;
+            if (2 * p + 1 < N) zs[(2 * p + 1) * RT + rr] = z1;
+        }
+    }
+#pragma unroll
+    for (int rr = 0; rr < RT; ++rr) {
+        const int r = r0 + rr;
+        if (gen[rr]) continue;
+        if (r >= a.K_loc) {
+            for (int t = tid; t < N; t += BLOCK) { zs[t * RT + rr] = 0.0; eps[t * RT + rr] = 0.0; }
+        } else if (a.zero_noise) {
+            // addExtraRollouts: noise = parameters - theta with parameters == theta, +0.0 exactly
+            for (int t = tid; t < N; t += BLOCK) {
+                eps[t * RT + rr] = 0.0;
+                a.noise[((size_t)r * J + d) * N + t] = 0.0;
+            }
+        } else {
+            // reused rollout: noise re-based on the current theta by the reuse kernel
+            for (int t = tid; t < N; t += BLOCK) eps[t * RT + rr] = a.noise[((size_t)r * J + d) * N + t];
+        }
+    }
+    __syncthreads();
+    STAMP(1);
+
+    // Loops run to a wave-uniform bound with clamped, unconditional loads so a lane's eight
+    // loads are in flight together.  The extra terms are exact no-ops: L^T is exactly zero
+    // above the diagonal (k > i) and past N the multiplier is forced to 0.0, and an
+    // accumulator that starts at +0.0 never becomes -0.0, so adding +-0.0 leaves it unchanged.
+    const int wave_end = min(N, __builtin_amdgcn_readfirstlane(tid & ~63) + 64);
+    if (any_gen && i < N) {
+        double acc[RT];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) acc[rr] = 0.0;
+        band_product<RT>(a.LT, N, i, wave_end, zs, acc);
+        const double th = a.theta[(size_t)d * N + i];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            if (!gen[rr]) continue;
+            const int r = r0 + rr;
+            const double e = sig * (0.0 + acc[rr]);
+            a.noise[((size_t)r * J + d) * N + i] = e;
+            a.params[((size_t)r * J + d) * N + i] = th + e;
+            eps[i * RT + rr] = e;
+        }
+    }
+    __syncthreads();
+    STAMP(2);
+
+    if (i < N) {
+        double acc[RT];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) acc[rr] = 0.0;
+        band_product<RT>(a.MT, N, i, N, eps, acc);
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            const int r = r0 + rr;
+            double p = 0.0;
+            if (r < a.K_loc) p = a.params[((size_t)r * J + d) * N + i];
+            xs[rr * Nall + i + 6] = p + acc[rr];
+        }
+    }
+    STAMP(3);
+    for (int idx = tid; idx < RT * 12; idx += BLOCK) {
+        const int rr = idx / 12, row = idx % 12;
+        xs[rr * Nall + (row < 6 ? row : N + row)] = row < 6 ? a.start[d] : a.goal[d];
+    }
+    __syncthreads();
+
+    for (int ii = tid; ii < Nall; ii += BLOCK) {
+        const int c0 = ii - 3 < 0 ? 0 : ii - 3;
+        const int c1 = ii + 3 >= Nall ? Nall - 1 : ii + 3;
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            double call = 0.0;
+#pragma unroll
+            for (int rule = 0; rule < 3; ++rule) {
+                const double wr = a.wr[rule];
+                if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
+                double s = 0.0;
+                for (int c = c0; c <= c1; ++c) s += a.dcoef[rule][c - ii + 3] * xs[rr * Nall + c];
+                call += wr * (s * s);
+            }
+            cs[rr * Nall + ii] = call;
+        }
+    }
+    __syncthreads();
+    STAMP(4);
+
+    if (i < N) {
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            const int r = r0 + rr;
+            if (r >= a.K_loc) continue;
+            const double* c = cs + rr * Nall;
+            double o = c[i + 6];
+            if (N == 1) {
+                for (int q = 0; q < 6; ++q) { o += c[q]; o += c[Nall - 1 - q]; }
+            } else if (i == 0) {
+                for (int q = 0; q < 6; ++q) o += c[q];
+            } else if (i == N - 1) {
+                for (int q = 0; q < 6; ++q) o += c[Nall - 1 - q];
+            }
+            a.control[((size_t)r * J + d) * N + i] = o;
+        }
+    }
+    STAMP(5);
+}
+
+STOMP_STAMP_ACCESSORS(noise)
+
+void launch_noise(const NoiseArgs& a, hipStream_t s)
+{
+    const int rows = a.K_loc - a.row_begin;
+    if (rows <= 0) return;
+    const int block = a.N <= 128 ? 128 : 256;
+    const int rt = rows >= 8 ? 8 : 1;
+    const size_t lds = (size_t)rt * (2 * a.N + 2 * a.Nall) * sizeof(double);
+    dim3 grid((rows + rt - 1) / rt, a.J);
+    if (rt == 8) {
+        if (block == 128) hipLaunchKernelGGL((k_noise<128, 8>), grid, dim3(128), lds, s, a);
+        else hipLaunchKernelGGL((k_noise<256, 8>), grid, dim3(256), lds, s, a);
+    } else {
+        if (block == 128) hipLaunchKernelGGL((k_noise<128, 1>), grid, dim3(128), lds, s, a);
+        else hipLaunchKernelGGL((k_noise<256, 1>), grid, dim3(256), lds, s, a);
+    }
+}
+
+}  // namespace stomp

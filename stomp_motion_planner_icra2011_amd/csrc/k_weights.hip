@@ -1,0 +1,270 @@
+// k_weights.hip -- exponentiated-cost probability weights and the weighted noise sum.
+//
+//   S[r,d,t]   = state[r,t] + control[r,d,t]  (or its suffix sum)   computeRolloutCumulativeCosts
+//                                                                   (policy_improvement.cpp:301-320)
+//   P[r,d,t]   = exp(-10 (S - min_r S) / max(max_r S - min_r S, 1e-8)) / sum_r (...)
+//                                                                   computeRolloutProbabilities (:322-368)
+//   u[d,t]     = sum_r eps[r,d,t] * P[r,d,t]                        computeParameterUpdates (:370-379)
+//
+// One workgroup owns TC time-step columns of one joint and stages the K_loc x TC cost tile
+// in LDS.  min/max are order-free; both sums use the canonical order (fixed 64-rollout
+// blocks summed sequentially, block partials summed in block order), which is what makes
+// the K-sharded multi-GPU result bit-identical to one GPU: the W_MINMAX / W_PSUM / W_USUM
+// phases emit exactly the per-block partials the fused mode sums, and RCCL moves them.
+#include "kernels.h"
+#include "stomp_math.h"
+#include "stamps.h"
+
+namespace stomp {
+
+// EPT: cost-tile elements per lane, K_loc * TC <= EPT * 256
+template <int EPT>
+__global__ __launch_bounds__(256) void k_weights(WeightArgs a)
+{
+    constexpr int BLOCK = 256;
+    extern __shared__ __attribute__((aligned(16))) double V[];   // K_loc * TC
+    __shared__ double red0[BLOCK], red1[BLOCK];
+    __shared__ double part[BLOCK];
+    __shared__ double mn_s[16], den_s[16], ps_s[16];
+    const int TC = a.tc, N = a.N, J = a.J, K = a.K_loc;
+    const int tid = threadIdx.x, c = tid % TC;
+    const int d = blockIdx.y, t0 = blockIdx.x * TC, t = t0 + c;
+    const bool colok = t < N;
+    const size_t JN = (size_t)J * N;
+    const size_t col = (size_t)d * N + t;
+    const size_t colc = (size_t)d * N + min(t, N - 1);   // clamped: loads stay unconditional
+    const int tcl = min(t, N - 1);
+    const int nel = K * TC;
+    const int nb = (K + kSumBlock - 1) / kSumBlock;
+    STAMP(0);
+
+    if (a.mode != W_USUM) {
+        double lmn = __builtin_inf(), lmx = -__builtin_inf();
+        // all of a lane's loads in flight together (nel <= EPT * BLOCK by weights_tile):
+        // clamped addresses, no loads under divergent branches
+        double v[EPT];
+        if (a.cum) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                const int r = min((tid + k * BLOCK) / TC, K - 1);
+                v[k] = a.cum[(size_t)r * JN + colc];
+            }
+        } else {
+            double w[EPT];
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                const int r = min((tid + k * BLOCK) / TC, K - 1);
+                v[k] = a.state[(size_t)r * N + tcl];
+                w[k] = a.control[(size_t)r * JN + colc];
+            }
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) v[k] += w[k];
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) v[k] = (tid + k * BLOCK < nel && colok) ? v[k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int el = tid + k * BLOCK;
+            if (el < nel) {
+                if (colok) {
+                    if (v[k] < lmn) lmn = v[k];
+                    if (v[k] > lmx) lmx = v[k];
+                }
+                V[el] = v[k];
+            }
+        }
+        if (a.mode == W_PSUM) {
+            if (tid < TC && colok) {
+                red0[tid] = -a.mm[JN + col];
+                red1[tid] = a.mm[col];
+            }
+        } else {
+            red0[tid] = lmn;
+            red1[tid] = lmx;
+            __syncthreads();
+            if (tid < TC) {
+                double mn = red0[tid], mx = red1[tid];
+                for (int j = tid + TC; j < BLOCK; j += TC) {
+                    if (red0[j] < mn) mn = red0[j];
+                    if (red1[j] > mx) mx = red1[j];
+                }
+                red0[tid] = mn;   // only lanes < TC read these slots from here on
+                red1[tid] = mx;
+                if (a.mode == W_MINMAX && colok) {
+                    a.mm[col] = mx;
+                    a.mm[JN + col] = -mn;
+                }
+            }
+            if (a.mode == W_MINMAX) return;
+        }
+        __syncthreads();
+        if (tid < TC) {
+            double den = red1[tid] - red0[tid];
+            if (den < 1e-8) den = 1e-8;
+            den_s[tid] = den;
+            mn_s[tid] = red0[tid];
+        }
+        __syncthreads();
+        STAMP(1);
+        for (int el = tid; el < nel; el += BLOCK) V[el] = det_exp(-10.0 * (V[el] - mn_s[c]) / den_s[c]);
+        __syncthreads();
+        STAMP(2);
+        if (tid < nb * TC) {
+            const int b = tid / TC, cc = tid % TC;
+            const int r1 = min(K, (b + 1) * kSumBlock);
+            double s = 0.0;
+            for (int r = b * kSumBlock; r < r1; ++r) s += V[r * TC + cc];
+            part[tid] = s;
+            if (a.mode == W_PSUM && t0 + cc < N) a.psum_part[(size_t)b * JN + (size_t)d * N + t0 + cc] = s;
+        }
+        if (a.mode == W_PSUM) {
+            for (int el = tid; el < nel; el += BLOCK)
+                if (colok) a.prob[(size_t)(el / TC) * JN + col] = V[el];
+            return;
+        }
+        __syncthreads();
+        if (tid < TC) {
+            double ps = 0.0;
+            for (int b = 0; b < nb; ++b) ps += part[b * TC + tid];
+            ps_s[tid] = ps;
+        }
+    } else {
+        double pv[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) pv[k] = a.prob[(size_t)min((tid + k * BLOCK) / TC, K - 1) * JN + colc];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k)
+            if (tid + k * BLOCK < nel) V[tid + k * BLOCK] = colok ? pv[k] : 0.0;
+        if (tid < TC) {
+            double ps = 0.0;
+            if (t0 + tid < N)
+                for (int b = 0; b < a.nb_total; ++b) ps += a.psum_all[(size_t)b * JN + (size_t)d * N + t0 + tid];
+            ps_s[tid] = ps;
+        }
+    }
+    __syncthreads();
+    STAMP(3);
+    {
+        double nz[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = min((tid + k * BLOCK) / TC, K - 1);
+            nz[k] = a.noise[(size_t)r * JN + colc];
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int el = tid + k * BLOCK;
+            if (el >= nel) continue;
+            if (!colok) { V[el] = 0.0; continue; }
+            const double pn = V[el] / ps_s[c];
+            a.prob[(size_t)(el / TC) * JN + col] = pn;
+            V[el] = nz[k] * pn;
+        }
+    }
+    __syncthreads();
+    if (tid < nb * TC) {
+        const int b = tid / TC, cc = tid % TC;
+        const int r1 = min(K, (b + 1) * kSumBlock);
+        double s = 0.0;
+        for (int r = b * kSumBlock; r < r1; ++r) s += V[r * TC + cc];
+        part[tid] = s;
+        if (a.mode == W_USUM && t0 + cc < N) a.u_part[(size_t)b * JN + (size_t)d * N + t0 + cc] = s;
+    }
+    if (a.mode == W_USUM) return;
+    __syncthreads();
+    STAMP(4);
+    if (tid < TC && colok) {
+        double u = 0.0;
+        for (int b = 0; b < nb; ++b) u += part[b * TC + tid];
+        a.u[col] = u;
+    }
+    STAMP(5);
+}
+
+STOMP_STAMP_ACCESSORS(weights)
+
+// columns per workgroup: as many as keep K_loc * TC <= 2048 (more workgroups, shorter
+// per-lane chains); K_loc in (2048, 4096] runs one column per workgroup with EPT = 16
+int weights_tile(int K_loc)
+{
+    int tc = 16;
+    while (tc > 1 && (size_t)K_loc * tc > 2048) tc >>= 1;
+    return tc;
+}
+
+void launch_weights(const WeightArgs& a, hipStream_t s)
+{
+    dim3 grid((a.N + a.tc - 1) / a.tc, a.J);
+    const size_t lds = (size_t)a.K_loc * a.tc * sizeof(double);
+    if ((size_t)a.K_loc * a.tc <= 2048)
+        hipLaunchKernelGGL((k_weights<8>), grid, dim3(256), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_weights<16>), grid, dim3(256), lds, s, a);
+}
+
+// computeRolloutCumulativeCosts with use_cumulative_costs (policy_improvement.cpp:308-316)
+__global__ void k_cumulative(WeightArgs a, double* cum)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.K_loc * a.J) return;
+    const int r = idx / a.J, d = idx % a.J;
+    const int N = a.N;
+    double* c = cum + ((size_t)r * a.J + d) * N;
+    const double* st = a.state + (size_t)r * N;
+    const double* ct = a.control + ((size_t)r * a.J + d) * N;
+    for (int t = 0; t < N; ++t) c[t] = st[t] + ct[t];
+    if (a.use_cumulative)
+        for (int t = N - 2; t >= 0; --t) c[t] += c[t + 1];
+}
+
+void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s)
+{
+    const int n = a.K_loc * a.J;
+    hipLaunchKernelGGL(k_cumulative, dim3((n + 255) / 256), dim3(256), 0, s, a, cum);
+}
+
+// delta = M u (policy_improvement.cpp:380), theta += 1.0 * delta (covariant_trajectory_policy.cpp:318-323).
+// With u_all (multi-GPU) u is first summed over the all-gathered block partials in block order.
+__global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
+                                                int nb_total, double* theta)
+{
+    __shared__ double us[256];
+    const int d = blockIdx.x, i = threadIdx.x;
+    const size_t JN = (size_t)J * N;
+    if (i < N) {
+        if (u_all) {
+            double s = 0.0;
+            for (int b = 0; b < nb_total; ++b) s += u_all[(size_t)b * JN + (size_t)d * N + i];
+            us[i] = s;
+        } else {
+            us[i] = u[(size_t)d * N + i];
+        }
+    }
+    __syncthreads();
+    if (i >= N) return;
+    // k ascending; clamped unconditional loads, the next 16 in flight while 16 are summed
+    constexpr int B = 16;
+    double s = 0.0;
+    double cur[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) cur[q] = MT[(size_t)min(q, N - 1) * N + i];
+    for (int k0 = 0; k0 < N; k0 += B) {
+        double nxt[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) nxt[q] = MT[(size_t)min(k0 + B + q, N - 1) * N + i];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+            if (k0 + q < N) s += cur[q] * us[k0 + q];
+#pragma unroll
+        for (int q = 0; q < B; ++q) cur[q] = nxt[q];
+    }
+    theta[(size_t)d * N + i] += 1.0 * s;
+}
+
+void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,
+                   hipStream_t s)
+{
+    hipLaunchKernelGGL(k_update, dim3(J), dim3(256), 0, s, J, N, MT, u, u_all, nb_total, theta);
+}
+
+}  // namespace stomp

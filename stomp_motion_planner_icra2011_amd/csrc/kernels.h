@@ -9,6 +9,7 @@
 //   control, prob    [K_loc][J][N]         fp64  Rollout::parameters_/noise_/control_costs_/probabilities_
 //   state            [K_loc][N]            fp64  Rollout::state_costs_
 //   sdf              [nx][ny][nz]          fp32  distance field (z fastest)
+//   psum/u partials  [blocks][J][N]        fp64  per-64-rollout-block sums (RCCL all-gather payload)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -17,9 +18,22 @@
 namespace stomp {
 
 constexpr int kMaxJoints = 32;
-constexpr int kRunMax = 12;      // spheres processed per FK op (LDS batch)
-constexpr int kSlots = 4;        // live FK frames per thread
-constexpr int kSumBlock = 64;    // canonical blocked summation over rollouts
+constexpr int kRunMaxSmall = 12;  // spheres per FK op when N <= 128 (LDS batch)
+constexpr int kRunMaxLarge = 8;   // spheres per FK op when N > 128
+constexpr int kSaves = 2;         // saved branch-point FK frames per thread (registers)
+constexpr int kSumBlock = 64;     // canonical blocked summation over rollouts
+constexpr int kVelTap0 = 2;       // non-zero taps of the velocity rule DIFF_RULES[0]
+constexpr int kVelTap1 = 5;       // (stomp_utils.h:54), checked in stomp_engine_create
+
+inline int run_max(int N) { return N <= 128 ? kRunMaxSmall : kRunMaxLarge; }
+
+// FK program step, executed by every waypoint lane (all fields wave-uniform):
+//   seg >= 0: C = base * pose(seg, q)   base: -2 = C itself (chain), -1 = identity (root),
+//                                        k >= 0 = saved frame k (branch point)
+//             if save >= 0: saved[save] = C
+//   then emit spheres [sph_begin, sph_end) from C (seg < 0: emit only).
+constexpr int kBaseChain = -2;
+constexpr int kBaseRoot = -1;
 
 struct DevSegment {
     int parent, q_index;
@@ -29,26 +43,26 @@ struct DevSegment {
 };
 
 struct DevSphere {
-    int segment, pad_;
+    int segment, slot;          // slot: index of its segment's published frame
     double radius, clearance, inv_clearance;
     double pos[3];
 };
 
-// One FK program step: frame[to] = frame[from] * pose(seg, q) (seg < 0: reuse frame `to`),
-// then emit spheres [sph_begin, sph_end) from frame[to].  from = -1: identity parent.
 struct FkOp {
-    int seg, from, to, sph_begin, sph_end;
+    int seg, base, save, sph_begin, sph_end;
+    int slot;                   // publish C as frame slot `slot` (-1: not a sphere segment)
 };
 
 struct DevModel {
-    int J, N, Nall, S, nops;
+    int J, N, Nall, S, nops, nseg, nslots, sph_chunk;
     const DevSegment* segs;
     const DevSphere* sph;
     const FkOp* ops;
+    const int* slot_sph;        // [nslots+1] spheres of slot g: [slot_sph[g], slot_sph[g+1])
     const double* pad_pos;      // [12][S][3]
     const float* sdf;
     int nx, ny, nz;
-    double ox, oy, oz, res;
+    double ox, oy, oz, res, inv_res;
     const double* start;        // [J]
     const double* goal;         // [J]
     double vel_coef[7];         // invTime * DIFF_RULES[0][k]
@@ -79,25 +93,54 @@ struct NoiseArgs {
     double* noise;
     double* control;
     int zero_noise;             // extra rollout: params given, noise = 0 (addExtraRollouts)
+    int row_begin;              // only rows [row_begin, K_loc) (reused rows after the reuse kernel)
 };
 
+// Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
+// x_params) evaluates the noiseless rollout of theta (pipelined from the previous iteration).
+struct CostArgs {
+    double* frames;             // [blocks][nslots][12][N] scratch between k_fk and k_pairs
+    const double* params;
+    long long stride;
+    int num_noisy;
+    int member;                 // StompOptimizer::iteration_ for the noisy rows
+    double* state_out;          // [num_noisy][N]
+    uint8_t* cf_out;            // [num_noisy] or null
+    double* traj_out;           // [num_noisy][J][N] or null
+    double* total_out;          // [num_noisy] or null
+    const double* x_params;     // [J][N] or null
+    int x_member;
+    double* x_state;
+    uint8_t* x_cf;
+    double* x_traj;
+    double* x_total;
+};
+
+enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
+
 struct WeightArgs {
-    int J, N, K_loc, use_cumulative;
+    int J, N, K_loc, use_cumulative, mode, tc, nb_total;
     const double* state;        // [K][N]
     const double* control;      // [K][J][N]
     const double* noise;        // [K][J][N]
-    double* cum;                // [K][J][N] scratch (cumulative costs) or null
+    const double* cum;          // [K][J][N] cumulative costs or null
     double* prob;               // [K][J][N]
-    double* u;                  // [J][N] reduced update (before projection)
+    double* u;                  // [J][N] reduced update before the projection (FUSED)
+    double* mm;                 // [2][J][N] (max, -min): MINMAX writes local, PSUM reads global
+    double* psum_part;          // [nb_loc][J][N]   PSUM writes
+    const double* psum_all;     // [nb_total][J][N] USUM reads
+    double* u_part;             // [nb_loc][J][N]   USUM writes
 };
 
-void launch_noise(const NoiseArgs& a, int rollouts_per_block, hipStream_t s);
-void launch_rollout_cost(const DevModel& m, const double* params, long long param_stride, int num,
-                         double* state_out, uint8_t* cf_out, double* traj_out, double* total_out,
-                         int iteration_member, hipStream_t s);
-void launch_cumulative(const WeightArgs& a, hipStream_t s);
+void launch_noise(const NoiseArgs& a, hipStream_t s);
+void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
+bool cost_supported(const DevModel& m);
+int pairs_sphere_chunk(int S, int N);
+void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
 void launch_weights(const WeightArgs& a, hipStream_t s);
-void launch_update(int J, int N, const double* MT, const double* u, double* theta, hipStream_t s);
+int weights_tile(int K_loc);
+void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
+                   double* theta, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);
 void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,

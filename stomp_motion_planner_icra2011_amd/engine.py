@@ -78,7 +78,7 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or _LIB_PATH
+    path = path or os.environ.get("STOMP_ENGINE_LIB") or _LIB_PATH
     if not os.path.exists(path):
         if os.path.exists(_build.HIPCC):
             _build.build()

@@ -399,7 +399,7 @@ def c_round(x):
 
 def sdf_lookup(p: Problem, pos: np.ndarray) -> np.ndarray:
     g = p.grid
-    f = c_round((pos - np.array(g.origin)) / g.resolution)
+    f = c_round((pos - np.array(g.origin)) * (1.0 / g.resolution))
     ok = np.all((f >= 1) & (f < g.n - 1), axis=-1)
     idx = np.where(ok[..., None], f, 0).astype(np.int64)
     d = p.sdf[idx[..., 0], idx[..., 1], idx[..., 2]].astype(np.float64)

@@ -1,0 +1,58 @@
+"""Diagnostic: per-phase cycle breakdown of the STOMP kernels from in-kernel s_memtime stamps.
+
+Needs the stamps library (python -m stomp_motion_planner_icra2011_amd._build --stamps); never
+used for timing claims (the stamps serialise the kernels they instrument).
+Usage: STOMP_ENGINE_LIB=.../libstomp_engine_stamps.so python tools/stamps.py [K] [grid]
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from stomp_motion_planner_icra2011_amd import engine as eng  # noqa: E402
+from stomp_motion_planner_icra2011_amd import problem as pb  # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+G = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+lib = eng.load_library()
+p = pb.make_problem(grid_n=G, num_rollouts=K, num_reused_rollouts=0, build_grid=False)
+sdf = eng.DeviceBuffer(4 * G ** 3)
+eng.sdf_build_device(p, sdf.ptr)
+e = eng.Engine(p, sdf_device_ptr=sdf.ptr)
+e.run(1, 5)
+e.synchronize()
+buf = (C.c_ulonglong * 256)()
+
+
+def show(name, block, labels):
+    fn = getattr(lib, "stomp_debug_stamps_" + name)
+    fn.argtypes = [C.c_int, C.c_void_p, C.c_int]
+    fn(block, None, 1)
+    e.run(6, 1)
+    e.synchronize()
+    fn(block, buf, 0)
+    v = np.array(buf[:], dtype=np.int64)
+    idx = [i for i in range(256) if v[i] != 0]
+    if not idx:
+        print(name, "no stamps")
+        return
+    t0 = v[idx[0]]
+    print(f"--- {name} block {block}: total {(v[idx[-1]] - t0)} cycles")
+    prev = t0
+    for i in idx:
+        print(f"  {labels(i):28s} +{v[i] - prev:8d}  @{v[i] - t0:8d}")
+        prev = v[i]
+
+
+def cost_label(i):
+    return {0: "fk: start", 1: "fk: tables loaded", 2: "fk: joint limits", 3: "fk: sincos", 4: "fk: frames",
+            100: "pairs: start", 101: "pairs: pos+gather", 102: "pairs: pot+vel", 103: "pairs: fold",
+            104: "pairs: end"}.get(i, str(i))
+
+
+show("cost", 0, cost_label)
+show("cost", K, cost_label)   # the pipelined noiseless rollout
+show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
+show("weights", 0, lambda i: ["start", "load+minmax", "exp", "psum", "u partials", "end"][i])
