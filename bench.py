@@ -11,8 +11,9 @@ the K dimension is sharded (K = 512 N, weak scaling) and the per-iteration
 reductions run over RCCL inside the engine.
 
 Also reported:
-  roofline      dominant kernel (rollout_cost): algorithmic bytes per launch
-                K_gen * N * (4 S + 8 J + 8) over its HIP-event duration in the timed region
+  roofline      dominant stage (rollout_cost = k_fk + k_pairs, Task::execute): algorithmic bytes
+                per launch (K_loc + 1) * N * (4 S + 8 J + 8) over its HIP-event duration, from a
+                second pass of the same K steps with events (the value pass has none)
   cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread)
                 timed on this host on a bounded sample of the same workload
 """
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--dof", type=int, default=7)
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--no-timing", action="store_true", help="no HIP events in the timed region")
+    ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event pass (no roofline)")
     return ap.parse_args()
 
 
@@ -94,7 +95,7 @@ def main():
 
     K = args.rollouts_per_gpu * world
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
-                        num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + args.steps + 1)
+                        num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + 2 * args.steps + 1)
     sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
     eng.sdf_build_device(p, sdf.ptr)
     comm_id = None
@@ -107,8 +108,6 @@ def main():
     # warmup
     e.run(1, args.warmup)
     e.synchronize()
-    if not args.no_timing:
-        e.set_timing(True)
     if dist:
         dist.barrier()
     e.synchronize()
@@ -127,8 +126,14 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = args.steps / elapsed
 
+    # Kernel durations: the same K steps again with HIP events recorded around every stage
+    # on the engine stream.  The events themselves cost ~10 us of dispatch gap per stage,
+    # which is why `value` comes from the event-free pass above.
     timing = {}
     if not args.no_timing:
+        e.set_timing(True)
+        e.run(args.warmup + args.steps + 1, args.steps)
+        e.synchronize()
         for name in ("noise", "rollout_cost", "weights", "update", "noiseless", "all"):
             tot, n = e.timing(name)
             timing[name] = {"total_ms": tot, "launches": n, "avg_us": 1000.0 * tot / max(n, 1)}
@@ -136,7 +141,8 @@ def main():
 
     S = len(p.spheres)
     K_loc = e.K_loc
-    bytes_per_launch = K_loc * p.N * (4 * S + 8 * p.J + 8)
+    # each launch evaluates K_loc noisy rollouts + the deferred noiseless rollout of theta
+    bytes_per_launch = (K_loc + 1) * p.N * (4 * S + 8 * p.J + 8)
     roofline = None
     if timing.get("rollout_cost", {}).get("launches"):
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6

@@ -18,7 +18,7 @@ BUILD = os.path.join(ROOT, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["k_noise.hip", "k_cost.hip", "k_weights.hip", "k_misc.hip", "selftest.hip", "engine.cpp", "setup.cpp"]
-HEADERS = ["kernels.h", "setup.h", "stomp_math.h", "device_fk.h"]
+HEADERS = ["kernels.h", "setup.h", "stomp_math.h", "device_fk.h", "stamps.h"]
 
 # One rounding per operation on host and device (parity with the oracle's FP contract).
 COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-Wall",
@@ -33,11 +33,13 @@ def _newer(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 4, variant: str = "") -> str:
-    """variant "stamps": diagnostic library with in-kernel phase stamps (libstomp_engine_stamps.so)."""
+def build(verbose: bool = False, force: bool = False, jobs: int = 4, variant: str = "", defines=()) -> str:
+    """variant "stamps": diagnostic library with in-kernel phase stamps (libstomp_engine_stamps.so);
+    any other variant name builds libstomp_engine_<name>.so with the extra -D `defines`
+    (experiments only: the product library is the plain build)."""
     os.makedirs(BUILD, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(INCLUDE, "stomp_engine.h")]
-    extra = ["-DSTOMP_STAMPS"] if variant == "stamps" else []
+    extra = (["-DSTOMP_STAMPS"] if variant == "stamps" else []) + list(defines)
     lib = LIB.replace(".so", "_" + variant + ".so") if variant else LIB
     suffix = ("." + variant) if variant else ""
     objs, procs = [], []
@@ -77,4 +79,9 @@ def _wait(procs):
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))
+    args = sys.argv[1:]
+    variant = "stamps" if "--stamps" in args else ""
+    if "--variant" in args:
+        variant = args[args.index("--variant") + 1]
+    defs = [a for a in args if a.startswith("-D")]
+    print(build(verbose=True, force="--force" in args or bool(defs), variant=variant, defines=defs))

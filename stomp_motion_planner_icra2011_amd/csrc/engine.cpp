@@ -589,7 +589,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     m.nslots = e->nslots;
     m.sph_chunk = pairs_sphere_chunk(std::max(e->S, 1), N);
     for (int g = 0; g < e->nslots; ++g) m.sph_chunk = std::max(m.sph_chunk, slot_sph[g + 1] - slot_sph[g]);
-    if ((size_t)m.sph_chunk * N * sizeof(double) + (size_t)e->S * sizeof(DevSphere) > 64 * 1024)
+    if (pairs_lds_bytes(m.sph_chunk, e->S, N) > 64 * 1024)
         CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "%d spheres on one segment x %d waypoints exceed the LDS budget",
                         m.sph_chunk, N));
     if (!cost_supported(m)) CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "FK program too large (%d ops, %d segments)",

@@ -2,8 +2,8 @@
 //
 // k_fk (one workgroup per rollout, lane t = free waypoint t):
 //   handleJointLimits (:562-616) on the LDS copy of the trajectory (block-wide "any
-//   violation" vote, then per limited joint a block-wide argmax with first-index tie break
-//   and a Q^-1 column axpy, <= 11 passes); sin/cos of every joint angle; the FK program
+//   violation" vote, then one wave per limited joint: wave argmax with first-index tie
+//   break and a Q^-1 column axpy, <= 11 passes); sin/cos of every joint angle; the FK program
 //   (treefksolverjointposaxis_partial.cpp:108-140 restated: one running frame plus <= 2
 //   saved branch frames in registers) and the frame of every sphere-carrying segment
 //   written to `frames` as [rollout][slot][component][t] (a wave's store = 512 contiguous B).
@@ -24,7 +24,10 @@ namespace stomp {
 namespace {
 constexpr int kMaxOps = 64;
 constexpr int kMaxSeg = 64;
-constexpr int kGather = 8;      // distance-field gathers in flight per lane
+#ifndef KGATHER
+#define KGATHER 8
+#endif
+constexpr int kGather = KGATHER;   // distance-field gathers in flight per lane
 constexpr int kPairsBlock = 256;
 }
 
@@ -36,8 +39,6 @@ __global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a)
     __shared__ DevSegment seg_s[kMaxSeg];
     __shared__ double jlim_s[2 * kMaxJoints];
     __shared__ int hl_s[kMaxJoints];
-    __shared__ double red_v[BLOCK / 64];
-    __shared__ int red_i[BLOCK / 64];
     constexpr int NW = BLOCK / 64;
     const int J = m.J, N = m.N;
     double* traj = lds;                          // J*N
@@ -69,20 +70,24 @@ __global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a)
         else if (v < jmin) absamt = fabs(jmin - v);
         any |= absamt > 1e-6;
     }
+    // Joints are independent, so each wave owns joints wv, wv + NW, ...: the argmax is a
+    // wave butterfly (every lane ends with the same (max, first index)) and a pass needs
+    // no block barrier.  LDS accesses of one wave execute in program order.
     if (__syncthreads_or(any)) {
-        for (int j = 0; j < J; ++j) {
+        for (int j = wv; j < J; j += NW) {
             if (!hl_s[j]) continue;
             const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
             const double* Q = m.QT + (size_t)j * N * N;
+            double* tj = traj + j * N;
             for (int pass = 0; pass < 11; ++pass) {
                 double cand = -1.0;
                 int ci = 0x7fffffff;
-                for (int t = tid; t < N; t += BLOCK) {
-                    const double v = traj[j * N + t];
-                    double amount = 0.0, absamt = 0.0;
-                    if (v > jmax) { amount = jmax - v; absamt = fabs(amount); }
-                    else if (v < jmin) { amount = jmin - v; absamt = fabs(amount); }
-                    if (absamt > 1e-6 && (absamt > cand || (absamt == cand && t < ci))) { cand = absamt; ci = t; }
+                for (int t = lane; t < N; t += 64) {
+                    const double v = tj[t];
+                    double absamt = 0.0;
+                    if (v > jmax) absamt = fabs(jmax - v);
+                    else if (v < jmin) absamt = fabs(jmin - v);
+                    if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
                 }
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) {
@@ -90,27 +95,15 @@ __global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a)
                     const int oi = __shfl_xor(ci, off, 64);
                     if (ov > cand || (ov == cand && oi < ci)) { cand = ov; ci = oi; }
                 }
-                if (lane == 0) { red_v[wv] = cand; red_i[wv] = ci; }
-                __syncthreads();
-                double bv = red_v[0];
-                int bi = red_i[0];
-                for (int w = 1; w < NW; ++w) {
-                    const double ov = red_v[w];
-                    const int oi = red_i[w];
-                    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-                }
-                double mult = 0.0;
-                if (bv >= 0.0) {
-                    const double v = traj[j * N + bi];
-                    const double amount = v > jmax ? jmax - v : jmin - v;
-                    mult = amount / Q[(size_t)bi * N + bi];
-                }
-                __syncthreads();   // red_v/red_i and traj[j][bi] consumed by every wave
-                if (bv < 0.0) break;
-                for (int t = tid; t < N; t += BLOCK) traj[j * N + t] += mult * Q[(size_t)bi * N + t];
-                __syncthreads();
+                if (cand < 0.0) break;   // wave-uniform
+                const double v = tj[ci];
+                const double amount = v > jmax ? jmax - v : jmin - v;
+                const double mult = amount / Q[(size_t)ci * N + ci];
+                for (int t = lane; t < N; t += 64) tj[t] += mult * Q[(size_t)ci * N + t];
+                __builtin_amdgcn_wave_barrier();
             }
         }
+        __syncthreads();
     }
     STAMP(2);
     double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
@@ -167,13 +160,15 @@ __global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
     const int N = m.N, S = m.S, G = m.nslots;
     const int SC = m.sph_chunk;                         // spheres per LDS chunk
     double* av = lds2;                                  // SC*N: pot, then a = pot*|v|
-    DevSphere* sph = (DevSphere*)(av + SC * N);         // S
+    double* pad = av + SC * N;                          // [12][S][3] padding-row positions
+    DevSphere* sph = (DevSphere*)(pad + 36 * S);        // S
     STAMP(100);
     const int e = blockIdx.x, tid = threadIdx.x;
     const bool extra = e == a.num_noisy;
     const int member = extra ? a.x_member : a.member;
     const double* frames = a.frames + (size_t)e * G * 12 * N;
     for (int idx = tid; idx < S; idx += BLOCK) sph[idx] = m.sph[idx];
+    for (int idx = tid; idx < 36 * S; idx += BLOCK) pad[idx] = m.pad_pos[idx];
     for (int idx = tid; idx <= G; idx += BLOCK) slot_sph_s[idx] = m.slot_sph[idx];
     if (tid == 0) flag = 0;
     __syncthreads();
@@ -191,8 +186,9 @@ __global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
             const int g = g0 + it / N, t = it - (it / N) * N;
             const int sb = slot_sph_s[g], se = slot_sph_s[g + 1];
             const double* fr = frames + (size_t)g * 12 * N;
-            double R[9], P[3];
-            load_frame(fr, N, t, R, P);
+            constexpr int NT = kVelTap1 - kVelTap0 + 1, TC = 3 - kVelTap0;   // TC: centre tap
+            double v[NT][12];
+            load_frame(fr, N, t, v[TC], v[TC] + 9);
             bool any = false;
             for (int q0 = sb; q0 < se; q0 += kGather) {
                 float dv[kGather];
@@ -200,8 +196,12 @@ __global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
                 for (int k = 0; k < kGather; ++k) {
                     const int s = min(q0 + k, se - 1);
                     double x[3];
-                    apply(R, P, sph[s].pos, x);
+                    apply(v[TC], v[TC] + 9, sph[s].pos, x);
+#ifdef PAIRS_NOGATHER
+                    dv[k] = (float)(x[0] + x[1]);
+#else
                     dv[k] = sdf_distance(m, x);
+#endif
                 }
 #pragma unroll
                 for (int k = 0; k < kGather; ++k) {
@@ -214,33 +214,33 @@ __global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
                     av[(s - s0) * N + t] = pot;   // a = pot * |v| is +0 exactly when pot == +0
                 }
             }
+#ifdef PAIRS_NOVEL
+            any = false;
+#endif
             if (any) {
-                // velocity stencil taps kVelTap0..kVelTap1 (the others are zero, checked on
-                // the host); the centre tap is the frame already in R, P
-                double v[kVelTap1 - kVelTap0 + 1][12];
+                // frames at the other velocity taps t-1, t+1, t+2 (kVelTap0..kVelTap1; the
+                // remaining taps are zero, checked on the host), clamped rows
 #pragma unroll
-                for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
-                    if (kk == 3) continue;
-                    const int tt = min(max(t + kk - 3, 0), N - 1);
-                    load_frame(fr, N, tt, v[kk - kVelTap0], v[kk - kVelTap0] + 9);
+                for (int q = 0; q < NT; ++q) {
+                    if (q == TC) continue;
+                    const int tt = min(max(t + q - TC, 0), N - 1);
+                    load_frame(fr, N, tt, v[q], v[q] + 9);
                 }
-#pragma unroll
-                for (int k = 0; k < 12; ++k) v[3 - kVelTap0][k] = k < 9 ? R[k] : P[k - 9];
                 for (int s = sb; s < se; ++s) {
                     const double pot = av[(s - s0) * N + t];
                     if (pot == 0.0) continue;
                     double v0 = 0.0, v1 = 0.0, v2 = 0.0;
 #pragma unroll
-                    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
-                        const double c = m.vel_coef[kk];
+                    for (int q = 0; q < NT; ++q) {
+                        const double c = m.vel_coef[kVelTap0 + q];
                         if (c == 0.0) continue;   // 0 * p adds a signed zero: |v| unchanged
-                        const int tt = t + kk - 3;
+                        const int tt = t + q - TC;
                         double y[3];
                         if (tt >= 0 && tt < N) {
-                            apply(v[kk - kVelTap0], v[kk - kVelTap0] + 9, sph[s].pos, y);
+                            apply(v[q], v[q] + 9, sph[s].pos, y);
                         } else {
                             const int row = tt < 0 ? tt + 6 : tt - N + 6;   // padding row 0..11
-                            const double* src = m.pad_pos + ((size_t)row * S + s) * 3;
+                            const double* src = pad + (row * S + s) * 3;
                             y[0] = src[0]; y[1] = src[1]; y[2] = src[2];
                         }
                         v0 += c * y[0];
@@ -288,10 +288,15 @@ STOMP_STAMP_ACCESSORS(cost)
 
 bool cost_supported(const DevModel& m) { return m.nops <= kMaxOps && m.nseg <= kMaxSeg && m.J <= kMaxJoints; }
 
+size_t pairs_lds_bytes(int chunk, int S, int N)
+{
+    return (size_t)chunk * N * sizeof(double) + (size_t)S * (36 * sizeof(double) + sizeof(DevSphere));
+}
+
 int pairs_sphere_chunk(int S, int N)
 {
-    // one double per (sphere, waypoint); chunk + sphere table within 64 KB of LDS
-    int sc = (int)((64 * 1024 - (size_t)S * sizeof(DevSphere)) / (8 * (size_t)N));
+    // one double per (sphere, waypoint); chunk + sphere tables within 64 KB of LDS
+    int sc = (int)((64 * 1024 - pairs_lds_bytes(0, S, N)) / (8 * (size_t)N));
     if (sc > S) sc = S;
     return sc < 1 ? 1 : sc;
 }
@@ -301,11 +306,10 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     const int blocks = a.num_noisy + (a.x_params ? 1 : 0);
     if (blocks <= 0) return;
     const size_t lds1 = (size_t)m.J * m.N * 3 * sizeof(double);
-    if (m.N <= 128)
-        hipLaunchKernelGGL((k_fk<128>), dim3(blocks), dim3(128), lds1, s, m, a);
-    else
-        hipLaunchKernelGGL((k_fk<256>), dim3(blocks), dim3(256), lds1, s, m, a);
-    const size_t lds2 = (size_t)m.sph_chunk * m.N * sizeof(double) + (size_t)m.S * sizeof(DevSphere);
+    // 256 lanes: four waves share the limited joints in handleJointLimits; the FK program
+    // runs on lanes t < N (N <= 256)
+    hipLaunchKernelGGL((k_fk<256>), dim3(blocks), dim3(256), lds1, s, m, a);
+    const size_t lds2 = pairs_lds_bytes(m.sph_chunk, m.S, m.N);
     hipLaunchKernelGGL((k_pairs<kPairsBlock>), dim3(blocks), dim3(kPairsBlock), lds2, s, m, a);
 }
 

@@ -136,6 +136,7 @@ void launch_noise(const NoiseArgs& a, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);
 int pairs_sphere_chunk(int S, int N);
+size_t pairs_lds_bytes(int chunk, int S, int N);
 void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
 void launch_weights(const WeightArgs& a, hipStream_t s);
 int weights_tile(int K_loc);
