@@ -22,6 +22,13 @@ DIFF_RULES = np.array([  # stomp_utils.h:49-56
     [0, 1 / 12.0, -17 / 12.0, 46 / 12.0, -46 / 12.0, 17 / 12.0, -1 / 12.0]])
 
 
+def potential(dist, radius, clearance):
+    """StompCollisionSpace::getCollisionPointPotentialGradient (stomp_collision_space.h:193-228)"""
+    d = np.asarray(dist, np.float64) - radius
+    c = clearance
+    return np.where(d >= c, 0.0, np.where(d >= 0.0, 0.5 * (d - c) ** 2 / c, -d + 0.5 * c))
+
+
 def diff_matrix(n: int, rule: np.ndarray, mult: float = 1.0) -> np.ndarray:
     """covariant_trajectory_policy.cpp:204-226 / stomp_cost.cpp:77-95"""
     D = np.zeros((n, n))
@@ -112,9 +119,7 @@ class NumpyStomp:
         for t in range(self.N):
             pos[6 + t] = pb.sphere_positions(p.robot, p.spheres, traj[:, t])
         dist = pb.sdf_lookup(p, pos[6:-6])
-        d = dist - self.radius[None, :]
-        c = self.clear[None, :]
-        pot = np.where(d >= c, 0.0, np.where(d >= 0.0, 0.5 * (d - c) ** 2 / c, -d + 0.5 * c))
+        pot = potential(dist, self.radius[None, :], self.clear[None, :])
         cf = not np.any(dist <= self.radius[None, :])
         if iteration_member == 0 and self.pad_collision:
             cf = False

@@ -1,0 +1,98 @@
+"""CPU tests of the drop-in boundary (include/stomp_engine.h): the HIP library
+loads without a GPU, exports every declared symbol, the ctypes mirror of every
+struct has the C layout, and argument validation fails loudly before any device
+call.  No compute runs here (no GPU in this container)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from stomp_motion_planner_icra2011_amd import engine as eng
+from stomp_motion_planner_icra2011_amd import problem as pb
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "stomp_engine.h")
+ORACLE_HEADER = os.path.join(ROOT, "oracle", "stomp_oracle.h")
+
+
+def declared_functions(path):
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b((?:stomp|so)_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_binding_list():
+    assert declared_functions(HEADER) == sorted(eng.EXPORTED)
+
+
+def test_engine_library_exports_every_symbol():
+    lib = eng.load_library()
+    missing = [f for f in declared_functions(HEADER) if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_oracle_library_exports_every_symbol():
+    from oracle import pyoracle as po
+    lib = po.lib()
+    missing = [f for f in declared_functions(ORACLE_HEADER) if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_struct_layouts_match_c(tmp_path):
+    structs = {"stomp_segment": eng.stomp_segment, "stomp_sphere": eng.stomp_sphere,
+               "stomp_joint": eng.stomp_joint, "stomp_grid": eng.stomp_grid,
+               "stomp_engine_desc": eng.stomp_engine_desc, "stomp_iter_out": eng.stomp_iter_out,
+               "stomp_stats": eng.stomp_stats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "stomp_engine.h"', "int main(void){"]
+    for name, cls in structs.items():
+        lines.append(f'printf("{name} %zu\\n", sizeof({name}));')
+        for field, _ in cls._fields_:
+            lines.append(f'printf("{name}.{field} %zu\\n", offsetof({name}, {field}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    out = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)], text=True).splitlines())
+    for name, cls in structs.items():
+        assert int(out[name]) == C.sizeof(cls), name
+        for field, _ in cls._fields_:
+            assert int(out[f"{name}.{field}"]) == getattr(cls, field).offset, f"{name}.{field}"
+
+
+def test_header_compiles_as_c_and_cpp(tmp_path):
+    src = tmp_path / "h.c"
+    src.write_text('#include "stomp_engine.h"\nint main(void){return STOMP_ENGINE_ABI_VERSION - 1;}\n')
+    for compiler, flag in (("gcc", "-std=c99"), ("g++", "-std=c++11")):
+        subprocess.check_call([compiler, flag, "-x", "c" if compiler == "gcc" else "c++", "-Wall", "-Werror",
+                               "-I", os.path.join(ROOT, "include"), str(src), "-o", str(tmp_path / "h")])
+
+
+@pytest.mark.parametrize("kw,code,msg", [
+    (dict(num_rollouts=10, num_reused_rollouts=10), -1, "strictly less"),
+    (dict(num_rollouts=10, num_reused_rollouts=0, torque_cost_weight=0.001), -3, "torque"),
+])
+def test_create_validates_before_touching_the_device(kw, code, msg):
+    p = pb.make_problem(grid_n=16, **kw)
+    with pytest.raises(RuntimeError) as ei:
+        eng.Engine(p)
+    assert f"error {code}" in str(ei.value) and msg in str(ei.value)
+
+
+def test_multi_rank_requires_whole_sum_blocks():
+    p = pb.make_problem(grid_n=16, num_rollouts=96, num_reused_rollouts=0)
+    with pytest.raises(RuntimeError) as ei:
+        eng.Engine(p, rank=0, world_size=2, comm_id=b"\0" * 128)
+    assert "multiple of 64" in str(ei.value)
+
+
+def test_abi_version_mismatch_rejected():
+    lib = eng.load_library()
+    d = eng.stomp_engine_desc()
+    d.abi_version = 999
+    h = C.c_void_p()
+    assert lib.stomp_engine_create(C.byref(d), C.byref(h)) == -1
+    assert b"abi_version" in lib.stomp_last_error()
+    assert not h.value

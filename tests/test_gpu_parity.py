@@ -164,3 +164,43 @@ def test_engine_on_device_sdf():
     o = po.Oracle(p)
     for it in range(1, 4):
         _compare_iteration(o, e, it)
+
+
+def _golden(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+
+
+def test_golden_cfg1_iterate_10_5():
+    g = _golden("cfg1_iterate_10_5")
+    e = eng.Engine(make(grid_n=128, K=10, Kr=5))
+    for it in range(1, 11):
+        c, cf = e.iterate(it)
+        assert c == g["costs"][it - 1] and cf == bool(g["cf"][it - 1])
+        np.testing.assert_array_equal(e.theta(), g["theta"][it - 1])
+    np.testing.assert_array_equal(e.rollouts("state_costs"), g["state_costs"])
+    np.testing.assert_array_equal(e.rollouts("probabilities"), g["probabilities"])
+
+
+def test_golden_cfg1_optimize():
+    # cfg1 (K = 20, K_r = 10, 128^3): the north-star check on best_group_trajectory_
+    g = _golden("cfg1_optimize_20_10")
+    e = eng.Engine(make(grid_n=128, K=20, Kr=10, max_iterations=100))
+    st, costs = e.optimize()
+    np.testing.assert_array_equal(costs, g["costs"])
+    best = e.best_trajectory()
+    np.testing.assert_array_equal(best, g["best"])
+    assert np.abs(best - g["best"]).max() <= TOL_FINAL
+    assert [st.iterations, st.success, st.success_iteration, st.collision_success_iteration,
+            st.last_improvement_iteration] == list(g["stats"])
+    assert st.best_cost == g["best_cost"][0]
+
+
+def test_golden_execute_cases():
+    g = _golden("execute_cases")
+    for dof in (7, 14):
+        e = eng.Engine(make(dof=dof, grid_n=64, K=10))
+        c, cf, tr = e.execute(g[f"params_{dof}"], 1)
+        np.testing.assert_array_equal(c, g[f"costs_{dof}"])
+        np.testing.assert_array_equal(tr, g[f"traj_{dof}"])
+        np.testing.assert_array_equal(cf, g[f"cf_{dof}"])
