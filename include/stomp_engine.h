@@ -165,7 +165,9 @@ int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
 /* Inspection for parity tests.  which: "params","noise","noise_projected"(if kept),
  * "control_costs","probabilities" -> K_local x J x N; "state_costs" -> K_local x N. */
 int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out);
-/* which: "Rinv","L","M","Qinv" (N x N, joint selects Qinv) */
+/* which: "Rinv","L","M","Qinv" (N x N, joint selects Qinv), "R" (free block of the
+ * control-cost matrix, CovariantTrajectoryPolicy::getControlCosts,
+ * covariant_trajectory_policy.h:235-239) */
 int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, double* out);
 /* sphere world positions at the 12 padding points (12 x S x 3) */
 int stomp_engine_get_pad_positions(stomp_engine* e, double* out);

@@ -1,0 +1,209 @@
+// stomp_facade.h -- C++ host API mirroring the reference's plugin/operator classes on the
+// hot path, forwarding to the MI355X engine through the C ABI (stomp_engine.h).
+//
+// Paths below are relative to /root/reference/stomp_motion_planner/.  Names, argument
+// meaning and the bool-return error convention follow the reference:
+//   Task                       include/stomp_motion_planner/task.h:49-93
+//   Policy                     include/stomp_motion_planner/policy.h:47-134
+//   CovariantTrajectoryPolicy  include/stomp_motion_planner/covariant_trajectory_policy.h:56-146
+//   PolicyImprovementLoop      include/stomp_motion_planner/policy_improvement_loop.h:52-98
+//   StompOptimizer             include/stomp_motion_planner/stomp_optimizer.h:63-213
+// What changes at the boundary (no ROS, Eigen 2, KDL or boost in this build):
+//   * Eigen::VectorXd -> VectorXd (std::vector<double>); Eigen::MatrixXd -> MatrixXd below
+//   * boost::shared_ptr -> std::shared_ptr; ros::NodeHandle arguments are dropped (the
+//     values the reference reads from the parameter server arrive in StompParameters)
+//   * the KDL tree / collision points / distance field arrive as plain tables
+//     (StompRobotModel, StompCollisionSpace), the ROS publishers and path constraints
+//     are not taken (the engine has no visualisation and no constraint term yet)
+// Failures return false and leave the reason in lastError() (the reference logs with
+// ROS_ERROR and returns false).  One optimizer owns one engine (one HIP device stream).
+#ifndef STOMP_MOTION_PLANNER_STOMP_FACADE_H
+#define STOMP_MOTION_PLANNER_STOMP_FACADE_H
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "stomp_engine.h"
+
+namespace stomp_motion_planner {
+
+using VectorXd = std::vector<double>;
+
+// Dense row-major matrix standing in for Eigen::MatrixXd at the API boundary.
+struct MatrixXd {
+    int rows_ = 0, cols_ = 0;
+    std::vector<double> data_;
+    MatrixXd() = default;
+    MatrixXd(int r, int c) : rows_(r), cols_(c), data_((size_t)r * c, 0.0) {}
+    int rows() const { return rows_; }
+    int cols() const { return cols_; }
+    double& operator()(int r, int c) { return data_[(size_t)r * cols_ + c]; }
+    double operator()(int r, int c) const { return data_[(size_t)r * cols_ + c]; }
+};
+
+// config/params.yaml + StompParameters (stomp_parameters.cpp:50-76)
+struct StompParameters {
+    double trajectory_duration = 5.0;
+    double trajectory_discretization = 0.05;
+    int max_iterations = 500;
+    int max_iterations_after_collision_free = 100;
+    double smoothness_cost_weight = 1e-6;
+    double obstacle_cost_weight = 1.0;
+    double constraint_cost_weight = 0.0;
+    double torque_cost_weight = 0.0;
+    double smoothness_cost_velocity = 0.0;
+    double smoothness_cost_acceleration = 1.0;
+    double smoothness_cost_jerk = 0.0;
+    double ridge_factor = 0.0;
+    bool use_cumulative_costs = false;
+    int num_rollouts = 10;
+    int num_reused_rollouts = 5;
+    std::vector<double> noise_stddev;   // per joint (policy_improvement_loop.cpp:99-100)
+    std::vector<double> noise_decay;    // per joint
+    uint64_t seed = 0x53544F4D50000000ull;
+};
+
+// StompRobotModel::StompPlanningGroup as the engine needs it: the kinematic tree in DFS
+// order, the planning-group joints and the collision points (stomp_robot_model.h).
+struct StompRobotModel {
+    std::vector<stomp_segment> segments;
+    std::vector<stomp_joint> joints;          // planning-group joints, J
+    std::vector<stomp_sphere> collision_points;
+};
+
+// StompCollisionSpace's distance field (stomp_collision_space.h:187-191).
+struct StompCollisionSpace {
+    stomp_grid grid{};
+};
+
+// StompTrajectory restricted to what optimize() reads and writes: the start / goal
+// configurations (the padding rows) and the free block, J x N row-major.
+struct StompTrajectory {
+    int num_joints = 0, num_points = 0;   // num_points = N free waypoints
+    VectorXd start, goal;                 // J
+    std::vector<VectorXd> free;           // [J] N: written by StompOptimizer::optimize()
+};
+
+class Policy {
+public:
+    virtual ~Policy() = default;
+    virtual bool setNumTimeSteps(const int num_time_steps) = 0;
+    virtual bool getNumTimeSteps(int& num_time_steps) = 0;
+    virtual bool getNumDimensions(int& num_dimensions) = 0;
+    virtual bool getNumParameters(std::vector<int>& num_params) = 0;
+    virtual bool getBasisFunctions(std::vector<MatrixXd>& basis_functions) = 0;
+    virtual bool getControlCosts(std::vector<MatrixXd>& control_costs) = 0;
+    virtual bool updateParameters(const std::vector<MatrixXd>& updates) = 0;
+    virtual bool getParameters(std::vector<VectorXd>& parameters) = 0;
+    virtual bool setParameters(const std::vector<VectorXd>& parameters) = 0;
+};
+
+class StompOptimizer;
+
+// The policy of one optimizer: theta lives in HBM inside the engine.
+class CovariantTrajectoryPolicy : public Policy {
+public:
+    explicit CovariantTrajectoryPolicy(StompOptimizer* owner) : owner_(owner) {}
+    bool setNumTimeSteps(const int num_time_steps) override;
+    bool getNumTimeSteps(int& num_time_steps) override;
+    bool getNumDimensions(int& num_dimensions) override;
+    bool getNumParameters(std::vector<int>& num_params) override;
+    bool getBasisFunctions(std::vector<MatrixXd>& basis_functions) override;
+    bool getControlCosts(std::vector<MatrixXd>& control_costs) override;
+    bool updateParameters(const std::vector<MatrixXd>& updates) override;
+    bool getParameters(std::vector<VectorXd>& parameters) override;
+    bool setParameters(const std::vector<VectorXd>& parameters) override;
+
+private:
+    StompOptimizer* owner_;
+};
+
+class Task {
+public:
+    virtual ~Task() = default;
+    virtual bool initialize(int num_time_steps) = 0;
+    virtual bool execute(std::vector<VectorXd>& parameters, VectorXd& costs, const int iteration_number) = 0;
+    virtual bool getPolicy(std::shared_ptr<Policy>& policy) = 0;
+    virtual bool setPolicy(const std::shared_ptr<Policy> policy) = 0;
+    virtual bool getControlCostWeight(double& control_cost_weight) = 0;
+};
+
+struct STOMPStatistics {   // msg/STOMPStatistics.msg without the ROS header / torques
+    int iterations = 0;
+    bool success = false;
+    int success_iteration = -1;
+    int collision_success_iteration = -1;
+    int last_improvement_iteration = -1;
+    double best_cost = 0.0;
+    std::vector<double> costs;   // last_trajectory_cost_ per iteration
+};
+
+class StompOptimizer : public Task {
+public:
+    // stomp_optimizer.cpp:50-70 (publishers and constraints not taken, see the file header)
+    StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model, const StompParameters* parameters,
+                   StompCollisionSpace* collision_space, int device = 0, void* stream = nullptr);
+    ~StompOptimizer() override;
+    StompOptimizer(const StompOptimizer&) = delete;
+    StompOptimizer& operator=(const StompOptimizer&) = delete;
+
+    // stomp_optimizer.cpp:249-401: runs the loop, writes best_group_trajectory_ back into
+    // the caller's trajectory; false if the engine failed (the reference returns void)
+    bool optimize();
+    const STOMPStatistics& getStatistics() const { return stats_; }
+
+    // Task (stomp_optimizer.cpp:1063-1165, 1167-1182)
+    bool initialize(int num_time_steps) override;
+    bool execute(std::vector<VectorXd>& parameters, VectorXd& costs, const int iteration_number) override;
+    bool getPolicy(std::shared_ptr<Policy>& policy) override;
+    bool setPolicy(const std::shared_ptr<Policy> policy) override;
+    bool getControlCostWeight(double& control_cost_weight) override;
+
+    // batched Task::execute: parameters [E][J] N -> costs [E] N, collision flags
+    bool executeBatch(const std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
+                      std::vector<bool>& collision_free, const int iteration_number);
+
+    bool ok() const { return engine_ != nullptr; }
+    const std::string& lastError() const { return error_; }
+    stomp_engine* engine() { return engine_; }
+    int numJoints() const { return J_; }
+    int numTimeSteps() const { return N_; }
+
+    // last_trajectory_cost_ / last_trajectory_collision_free_ after runSingleIteration
+    double lastTrajectoryCost() const { return last_cost_; }
+    bool lastTrajectoryCollisionFree() const { return last_cf_; }
+
+private:
+    friend class PolicyImprovementLoop;
+    friend class CovariantTrajectoryPolicy;
+    bool check(int rc);
+    StompTrajectory* trajectory_;
+    const StompParameters* parameters_;
+    stomp_engine* engine_ = nullptr;
+    std::shared_ptr<Policy> policy_;
+    int J_ = 0, N_ = 0;
+    double last_cost_ = 0.0;
+    bool last_cf_ = false;
+    STOMPStatistics stats_;
+    std::string error_;
+};
+
+// policy_improvement_loop.cpp:88-202.  The loop drives the engine's fused iteration, so
+// the task must be a StompOptimizer (the reference loop only ever runs that task).
+class PolicyImprovementLoop {
+public:
+    bool initialize(std::shared_ptr<Task> task);
+    bool runSingleIteration(int iteration_number);
+    const std::string& lastError() const { return error_; }
+
+private:
+    std::shared_ptr<Task> task_;
+    StompOptimizer* optimizer_ = nullptr;
+    std::string error_;
+};
+
+}  // namespace stomp_motion_planner
+
+#endif

@@ -67,6 +67,26 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4, variant: st
     return lib
 
 
+FACADE_SRC = os.path.join(PKG, "facade", "stomp_facade.cpp")
+FACADE_LIB = os.path.join(PKG, "libstomp_facade.so")
+FACADE_HDR = os.path.join(INCLUDE, "stomp_motion_planner", "stomp_facade.h")
+
+
+def build_facade(verbose: bool = False, force: bool = False) -> str:
+    """libstomp_facade.so: the reference-shaped C++ classes over the C ABI (host code only)."""
+    lib = build(verbose=verbose)
+    deps = [FACADE_SRC, FACADE_HDR, os.path.join(INCLUDE, "stomp_engine.h"), lib]
+    if force or _newer(FACADE_LIB, deps):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + INCLUDE, FACADE_SRC, "-o", FACADE_LIB,
+               "-L" + PKG, "-l:libstomp_engine.so", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("facade build failed:\n" + r.stdout)
+    return FACADE_LIB
+
+
 def _wait(procs):
     errs = []
     for cmd, p in procs:
@@ -85,3 +105,5 @@ if __name__ == "__main__":
         variant = args[args.index("--variant") + 1]
     defs = [a for a in args if a.startswith("-D")]
     print(build(verbose=True, force="--force" in args or bool(defs), variant=variant, defines=defs))
+    if not variant:
+        print(build_facade(verbose=True, force="--force" in args))

@@ -801,7 +801,12 @@ int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, d
     if (!std::strcmp(which, "Rinv")) std::memcpy(out, e->su.Rinv.data(), NN * 8);
     else if (!std::strcmp(which, "L")) std::memcpy(out, e->su.L.data(), NN * 8);
     else if (!std::strcmp(which, "M")) std::memcpy(out, e->su.M.data(), NN * 8);
-    else if (!std::strcmp(which, "Qinv")) {
+    else if (!std::strcmp(which, "R")) {
+        // free block of the control-cost matrix (CovariantTrajectoryPolicy::getControlCosts)
+        for (int i = 0; i < e->N; ++i)
+            for (int k = 0; k < e->N; ++k)
+                out[(size_t)i * e->N + k] = e->su.Rall[(size_t)(i + kPad) * e->Nall + k + kPad];
+    } else if (!std::strcmp(which, "Qinv")) {
         if (joint < 0 || joint >= e->J) return fail(e, STOMP_E_INVALID, "joint out of range");
         std::memcpy(out, e->su.Qinv.data() + (size_t)joint * NN, NN * 8);
     } else return fail(e, STOMP_E_INVALID, "unknown matrix '%s'", which);
