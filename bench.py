@@ -149,8 +149,13 @@ def main():
         achieved = bytes_per_launch / avg_s / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": latest_traffic(),
-                    "kernel": "k_rollout_cost", "bytes_per_launch": bytes_per_launch,
+                    "kernel": "rollout_cost (k_fk + k_pairs)", "bytes_per_launch": bytes_per_launch,
                     "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3)}
+    if roofline is not None:
+        # whole iteration, B_iter = E * N * (4 S + 16 J + 8), E = K + 1, all ranks
+        b_iter = (K + 1) * p.N * (4 * S + 16 * p.J + 8)
+        roofline["iteration_bytes"] = b_iter
+        roofline["iteration_frac"] = round(b_iter * value / (HBM_PEAK_GBS * 1e9 * world), 5)   # vs N x peak
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
