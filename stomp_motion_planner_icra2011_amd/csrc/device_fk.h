@@ -115,7 +115,9 @@ __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* _
     const double fz = round((p[2] - m.oz) * m.inv_res);
     const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
                     fz < (double)(m.nz - 1);
-    const size_t idx = ok ? ((size_t)(int)fx * m.ny + (size_t)(int)fy) * m.nz + (size_t)(int)fz : 0;
+    // in range the coordinates are small non-negative integers; the cell index fits 32 bits
+    // (checked at engine creation)
+    const unsigned idx = ok ? ((unsigned)fx * (unsigned)m.ny + (unsigned)fy) * (unsigned)m.nz + (unsigned)fz : 0u;
     const float v = m.sdf[idx];
     return ok ? v : 0.0f;
 }

@@ -52,8 +52,6 @@ struct stomp_engine {
     std::vector<FkOp> ops;
     std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
     int nslots = 0;
-    double* d_frames = nullptr;     // [frames_cap][nslots][12][N]
-    int frames_cap = 0;
     std::vector<void*> allocs;
     double *d_theta = nullptr, *d_LT = nullptr, *d_MT = nullptr, *d_QT = nullptr;
     double *d_params = nullptr, *d_noise = nullptr, *d_control = nullptr, *d_prob = nullptr, *d_state = nullptr;
@@ -267,7 +265,6 @@ void launch_noiseless(stomp_engine* e, int member)
 {
     Timed tm(e, T_NOISELESS);
     CostArgs ca{};
-    ca.frames = e->d_frames;
     ca.num_noisy = 0;
     ca.x_params = e->d_theta; ca.x_member = member;
     ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
@@ -330,8 +327,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     {
         const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
         CostArgs ca{};
-        ca.frames = e->d_frames;
-        ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = std::max(g1 - g0, 0);
+            ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = std::max(g1 - g0, 0);
         ca.member = member; ca.state_out = e->d_state;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
@@ -422,6 +418,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         return fail(nullptr, STOMP_E_INVALID, "missing table pointer");
     if (d->grid.nx < 3 || d->grid.ny < 3 || d->grid.nz < 3 || !(d->grid.resolution > 0))
         return fail(nullptr, STOMP_E_INVALID, "invalid grid");
+    if ((uint64_t)d->grid.nx * (uint64_t)d->grid.ny * (uint64_t)d->grid.nz > 0xFFFFFFFFull)
+        return fail(nullptr, STOMP_E_UNSUPPORTED, "distance field larger than 2^32 cells");
     for (int s = 0; s < d->num_segments; ++s)
         if (d->segments[s].parent >= s || d->segments[s].q_index >= d->num_joints)
             return fail(nullptr, STOMP_E_INVALID, "segment %d: parent must precede it (DFS order), q_index < J", s);
@@ -558,8 +556,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
     if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
-    e->frames_cap = e->K_loc + 1;
-    CREATE_TRY(dev_alloc(e, &e->d_frames, (size_t)e->frames_cap * std::max(e->nslots, 1) * 12 * N));
     if (world > 1) {
         const size_t nb_loc = (size_t)e->K_loc / kSumBlock, nb_tot = (size_t)e->K / kSumBlock;
         CREATE_TRY(dev_alloc(e, &e->d_mm, 2 * (size_t)J * N));
@@ -587,11 +583,25 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     DevModel& m = e->model;
     m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size(); m.nseg = e->nseg;
     m.nslots = e->nslots;
-    m.sph_chunk = pairs_sphere_chunk(std::max(e->S, 1), N);
+    m.sph_chunk = 1;   // the per-slot a buffer holds the largest slot
     for (int g = 0; g < e->nslots; ++g) m.sph_chunk = std::max(m.sph_chunk, slot_sph[g + 1] - slot_sph[g]);
-    if (pairs_lds_bytes(m.sph_chunk, e->S, N) > 64 * 1024)
-        CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "%d spheres on one segment x %d waypoints exceed the LDS budget",
-                        m.sph_chunk, N));
+    {
+        if (m.sph_chunk * N > 65535)
+            CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "%d spheres on one segment x %d waypoints exceed 16-bit pair ids",
+                            m.sph_chunk, N));
+        m.nsaves = 0;
+        for (const FkOp& o : e->ops) m.nsaves = std::max(m.nsaves, o.save + 1);
+        // padding-row positions go to LDS only when that costs no workgroup per CU
+        const size_t stat = rollout_static_lds();
+        const size_t with_pad = rollout_lds_bytes(m, 1) + stat, without = rollout_lds_bytes(m, 0) + stat;
+        m.pad_lds = (with_pad <= kRolloutLdsMax &&
+                     rollout_blocks_per_cu(with_pad) >= rollout_blocks_per_cu(without)) ? 1 : 0;
+        const size_t lds = rollout_lds_bytes(m, m.pad_lds) + stat;
+        if (lds > kRolloutLdsMax)
+            CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
+                                                    "on one segment), more than %zu", lds, J, N, e->S, m.sph_chunk,
+                            kRolloutLdsMax));
+    }
     if (!cost_supported(m)) CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "FK program too large (%d ops, %d segments)",
                                             m.nops, m.nseg));
     m.segs = d_segs; m.sph = d_sph; m.ops = d_ops; m.slot_sph = d_slot_sph; m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
@@ -701,17 +711,8 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
         if ((rc = dev_alloc(e, &e->d_eval_cf, (size_t)num))) return rc;
         e->eval_cap = num;
     }
-    if (num > e->frames_cap) {
-        HIP_TRY(e, hipStreamSynchronize(e->stream));
-        hipFree(e->d_frames);
-        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), (void*)e->d_frames), e->allocs.end());
-        int rc;
-        if ((rc = dev_alloc(e, &e->d_frames, (size_t)num * std::max(e->nslots, 1) * 12 * e->N))) return rc;
-        e->frames_cap = num;
-    }
     HIP_TRY(e, hipMemcpyAsync(e->d_eval_params, params, sizeof(double) * num * JN, hipMemcpyHostToDevice, e->stream));
     CostArgs ca{};
-    ca.frames = e->d_frames;
     ca.params = e->d_eval_params; ca.stride = (long long)JN; ca.num_noisy = num; ca.member = iteration_member;
     ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf; ca.traj_out = traj_out ? e->d_eval_traj : nullptr;
     launch_cost(e->model, ca, e->stream);

@@ -1,19 +1,22 @@
-// k_cost.hip -- StompOptimizer::execute (stomp_optimizer.cpp:1063-1165) as two launches.
+// k_cost.hip -- StompOptimizer::execute (stomp_optimizer.cpp:1063-1165), one workgroup per rollout.
 //
-// k_fk (one workgroup per rollout, lane t = free waypoint t):
-//   handleJointLimits (:562-616) on the LDS copy of the trajectory (block-wide "any
-//   violation" vote, then one wave per limited joint: wave argmax with first-index tie
-//   break and a Q^-1 column axpy, <= 11 passes); sin/cos of every joint angle; the FK program
-//   (treefksolverjointposaxis_partial.cpp:108-140 restated: one running frame plus <= 2
-//   saved branch frames in registers) and the frame of every sphere-carrying segment
-//   written to `frames` as [rollout][slot][component][t] (a wave's store = 512 contiguous B).
-// k_pairs (one workgroup per rollout, one lane per (frame slot, waypoint) over 256 lanes):
-//   sphere position (stomp_collision_point.h:138-141), distance-field gather and hinge
-//   potential (stomp_optimizer.cpp:659-674, stomp_collision_space.h:193-228); where the
-//   potential is non-zero the 7-tap velocity (:683-698; the t-3, t-2, t+3 taps are zero,
-//   padding rows come from the iteration-0 FK of start/goal) -> a = pot * |v| (pot == +0
-//   gives +0 exactly, as the reference's product does); then lane t folds a over the
-//   spheres in list order into cum / state (:1096-1105) and writes the state cost.
+// k_rollout<256>, everything in LDS, nothing but the inputs and the state costs touches HBM:
+//   1. handleJointLimits (:562-616) on the LDS copy of the trajectory: block-wide "any
+//      violation" vote, then one wave per limited joint (wave argmax with first-index tie
+//      break, Q^-1 column axpy, <= 11 passes).
+//   2. The FK program (treefksolverjointposaxis_partial.cpp:108-140 restated: one running
+//      frame in the registers of lanes t < N, <= 2 saved branch frames in LDS) walks the
+//      segments in DFS order.  Each sphere-carrying segment ("slot") is published to an LDS
+//      frame buffer [12][N]; then lane (t, g) reads the frame at t once and takes spheres
+//      g, g + G, ... of the slot (G = 256 / N groups): sphere position
+//      (stomp_collision_point.h:138-141), distance-field gathers (branch-free, 4 in flight
+//      per lane) and hinge potential (stomp_optimizer.cpp:659-674,
+//      stomp_collision_space.h:193-228); where the potential is non-zero, the 7-tap
+//      velocity (:683-698) from the neighbouring frames in LDS (padding rows: iteration-0
+//      FK of start/goal) and a = pot * |v|; then lanes t fold a over the slot's spheres,
+//      in list order, into cum / state (:1096-1105).  Slots are numbered in sphere order,
+//      so slot-by-slot folding is the reference's order.
+//   3. costs(t) = w_obs * state (:1148-1151), the collision flag and the total (:1155).
 // The extra workgroup (index num_noisy) evaluates the noiseless rollout of theta that the
 // previous iteration deferred (policy_improvement_loop.cpp:180-182).
 #include "device_fk.h"
@@ -24,38 +27,120 @@ namespace stomp {
 namespace {
 constexpr int kMaxOps = 64;
 constexpr int kMaxSeg = 64;
-#ifndef KGATHER
-#define KGATHER 8
+constexpr int kBlock = 256;
+#ifndef ROLLOUT_MIN_WAVES
+#define ROLLOUT_MIN_WAVES 3
 #endif
-constexpr int kGather = KGATHER;   // distance-field gathers in flight per lane
-constexpr int kPairsBlock = 256;
+#ifndef PAIR_UNROLL
+#define PAIR_UNROLL 4
+#endif
+constexpr int kPairUnroll = PAIR_UNROLL;   // spheres per lane with gathers in flight   // (sphere, waypoint) pairs per lane in flight
+}
+
+__device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
+{
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        x[i] = fb[(3 * i + 0) * N + t] * pos[0] + fb[(3 * i + 1) * N + t] * pos[1] +
+               fb[(3 * i + 2) * N + t] * pos[2] + fb[(9 + i) * N + t];
+}
+
+// |v| of sphere s at free waypoint t: the 7-tap velocity of its position (stomp_optimizer.cpp:683-698)
+// from the slot's frames in LDS, padding rows from the iteration-0 FK of start / goal
+__device__ __forceinline__ double sphere_speed(const DevModel& m, const double* fb, const double* pad,
+                                               const DevSphere& sp, int s, int t)
+{
+    const int N = m.N;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+#pragma unroll
+    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
+        const double c = m.vel_coef[kk];
+        if (c == 0.0) continue;   // 0 * p adds a signed zero: |v| unchanged
+        const int tt = t + kk - 3;
+        double y[3];
+        if (tt >= 0 && tt < N) {
+            apply_lds(fb, N, tt, sp.pos, y);
+        } else {
+            const int row = tt < 0 ? tt + 6 : tt - N + 6;   // padding row 0..11
+            const double* src = pad + (row * m.S + s) * 3;
+            y[0] = src[0]; y[1] = src[1]; y[2] = src[2];
+        }
+        v0 += c * y[0];
+        v1 += c * y[1];
+        v2 += c * y[2];
+    }
+    return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+}
+
+// LDS carve-up (bytes), shared with the host-side size check
+struct RolloutLds {
+    size_t sc, traj, fb, sv, av, nzl, sph, seg, ops, pad, total;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// traj stays resident (the FK lanes take sin/cos of their own joint values as they go);
+// the per-slot buffers follow it
+__host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_slot, int nsaves, int nseg, int nops,
+                                                  int pad_lds)
+{
+    RolloutLds l;
+    l.sc = 0;   // unused: no sin/cos table
+    l.traj = 0;
+    l.fb = l.traj + (size_t)J * N * sizeof(double);
+    l.sv = l.fb + (size_t)12 * N * sizeof(double);
+    l.av = l.sv + (size_t)nsaves * 12 * N * sizeof(double);
+    l.nzl = l.av + (size_t)max_slot * N * sizeof(double);
+    l.sph = align16(l.nzl + (size_t)max_slot * N * sizeof(unsigned short));
+    l.seg = align16(l.sph + (size_t)S * sizeof(DevSphere));
+    l.ops = align16(l.seg + (size_t)nseg * sizeof(DevSegment));
+    l.pad = align16(l.ops + (size_t)nops * sizeof(FkOp));
+    l.total = l.pad + (pad_lds ? (size_t)36 * S * sizeof(double) : 0);
+    return l;
 }
 
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a)
+__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
 {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    __shared__ FkOp ops_s[kMaxOps];
-    __shared__ DevSegment seg_s[kMaxSeg];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    __shared__ int slot_sph_s[kMaxSeg + 1];
     __shared__ double jlim_s[2 * kMaxJoints];
     __shared__ int hl_s[kMaxJoints];
-    constexpr int NW = BLOCK / 64;
-    const int J = m.J, N = m.N;
-    double* traj = lds;                          // J*N
-    double* sc = traj + J * N;                   // J*N*2 (sin, cos)
+    __shared__ int flag;
+    __shared__ int nz_count;
+    const int J = m.J, N = m.N, S = m.S;
+    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.pad_lds);
+    double* traj = (double*)(lds_raw + L.traj);   // J*N
+    double* fb = (double*)(lds_raw + L.fb);       // 12*N frame of the current slot
+    double* sv = (double*)(lds_raw + L.sv);       // nsaves*12*N saved branch-point frames
+    double* av = (double*)(lds_raw + L.av);
+    unsigned short* nzl = (unsigned short*)(lds_raw + L.nzl);   // pairs q*N+t with a non-zero potential       // max_slot*N: pot, then pot * |v|
+    DevSphere* sph = (DevSphere*)(lds_raw + L.sph);
+    DevSegment* seg_s = (DevSegment*)(lds_raw + L.seg);
+    FkOp* ops_s = (FkOp*)(lds_raw + L.ops);
+    // [12][S][3] padding-row sphere positions: LDS copy when it fits, else HBM
+    const double* pad = m.pad_lds ? (const double*)(lds_raw + L.pad) : m.pad_pos;
 
     STAMP(0);
+    BLOCK_BEGIN();
     const int e = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = BLOCK / 64;
     const bool extra = e == a.num_noisy;
+    const int member = extra ? a.x_member : a.member;
     const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
     for (int idx = tid; idx < J * N; idx += BLOCK) traj[idx] = prm[idx];
     for (int idx = tid; idx < m.nops; idx += BLOCK) ops_s[idx] = m.ops[idx];
     for (int idx = tid; idx < m.nseg; idx += BLOCK) seg_s[idx] = m.segs[idx];
+    for (int idx = tid; idx <= m.nslots; idx += BLOCK) slot_sph_s[idx] = m.slot_sph[idx];
+    for (int idx = tid; idx < S; idx += BLOCK) sph[idx] = m.sph[idx];
+    if (m.pad_lds)
+        for (int idx = tid; idx < 36 * S; idx += BLOCK) ((double*)(lds_raw + L.pad))[idx] = m.pad_pos[idx];
     for (int idx = tid; idx < J; idx += BLOCK) {
         hl_s[idx] = m.has_limits[idx];
         jlim_s[2 * idx] = m.jmin[idx];
         jlim_s[2 * idx + 1] = m.jmax[idx];
     }
+    if (tid == 0) flag = 0;
     __syncthreads();
     STAMP(1);
 
@@ -109,165 +194,137 @@ __global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a)
     double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
     if (tout)
         for (int idx = tid; idx < J * N; idx += BLOCK) tout[idx] = traj[idx];
-    for (int idx = tid; idx < J * N; idx += BLOCK) det_sincos(traj[idx], &sc[2 * idx], &sc[2 * idx + 1]);
     __syncthreads();
     STAMP(3);
 
-    if (tid < N) {
-        const int t = tid;
-        double* fout = a.frames + (size_t)e * m.nslots * 12 * N;
-        Frame C, S0, S1;
-        for (int op = 0; op < m.nops; ++op) {
-            const FkOp o = ops_s[op];
-            if (o.seg < 0) continue;   // emit-only step: same frame as the step before
+    // ---- FK program, slot by slot, with the slot's pairs in between
+    const int t_own = tid;                      // FK / fold lane: waypoint tid (tid < N)
+    const int qb = tid / N, tb = tid - qb * N;  // first (sphere, waypoint) pair of this lane
+    const int dq = BLOCK / N, dt = BLOCK - dq * N;
+    // C: running frame in the registers of lanes t < N, reloaded from fb after each slot's
+    // pairs so it is not live across them; branch-point frames saved in LDS (column t of sv)
+    Frame C;
+    double cum = 0.0, state = 0.0;
+    bool col = false;
+    for (int op = 0; op < m.nops; ++op) {
+        const FkOp o = ops_s[op];
+        if (o.seg >= 0 && t_own < N) {
             const DevSegment& sg = seg_s[o.seg];
             double st = 0.0, ct = 1.0;
-            if (sg.q_index >= 0) {
-                st = sc[2 * (sg.q_index * N + t)];
-                ct = sc[2 * (sg.q_index * N + t) + 1];
-            }
-            fk_op(sg, o.base, o.save, st, ct, C, S0, S1);
-            if (o.slot >= 0) {
-                double* f = fout + (size_t)o.slot * 12 * N + t;
+            if (sg.q_index >= 0) det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
+            Frame nf;
+            if (o.base == kBaseChain) {
+                compose(sg, &C, st, ct, nf);
+            } else if (o.base == kBaseRoot) {
+                compose(sg, nullptr, st, ct, nf);
+            } else {
+                Frame pf;
+                const double* src = sv + (size_t)o.base * 12 * N + t_own;
 #pragma unroll
-                for (int k = 0; k < 9; ++k) f[k * N] = C.R[k];
+                for (int k = 0; k < 9; ++k) pf.R[k] = src[k * N];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) f[(9 + k) * N] = C.p[k];
+                for (int k = 0; k < 3; ++k) pf.p[k] = src[(9 + k) * N];
+                compose(sg, &pf, st, ct, nf);
             }
+            C = nf;
+            if (o.save >= 0) {
+                double* dst = sv + (size_t)o.save * 12 * N + t_own;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) dst[k * N] = C.R[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
+            }
+        }
+        if (o.slot < 0) continue;   // uniform: not a sphere-carrying segment
+        if (t_own < N) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) fb[k * N + t_own] = C.R[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) fb[(9 + k) * N + t_own] = C.p[k];
+        }
+        if (tid == 0) nz_count = 0;
+        __syncthreads();   // frame published; every lane's previous fold is done
+        STAMP(10 + 2 * o.slot);
+        const int sb = slot_sph_s[o.slot], se = slot_sph_s[o.slot + 1];
+        // lane = consecutive (sphere, waypoint) pairs of the slot, kPairUnroll in flight
+        // lane takes pairs (q, t) = (tid / N, tid % N) + k * BLOCK, stepped without dividing
+        const int ns = se - sb;
+        int q = qb, t = tb;
+        while (q < ns) {
+            int qq[kPairUnroll], tt[kPairUnroll];
+            float dv[kPairUnroll];
+#pragma unroll
+            for (int u = 0; u < kPairUnroll; ++u) {
+                qq[u] = q;
+                tt[u] = t;
+                q += dq;
+                t += dt;
+                if (t >= N) { t -= N; ++q; }
+            }
+#pragma unroll
+            for (int u = 0; u < kPairUnroll; ++u) {
+                double x[3];
+                apply_lds(fb, N, tt[u], sph[sb + min(qq[u], ns - 1)].pos, x);
+                dv[u] = sdf_distance(m, x);
+            }
+#pragma unroll
+            for (int u = 0; u < kPairUnroll; ++u) {
+                const bool in = qq[u] < ns;
+                double pot = 0.0;
+                if (in) {
+                    const DevSphere& sp = sph[sb + qq[u]];
+                    const double dd = (double)dv[u];
+                    col |= dd <= sp.radius;
+                    pot = potential(sp, dd);
+                    av[qq[u] * N + tt[u]] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                }
+#ifndef NO_COMPACT
+                // append (q, t) with pot != 0 to the slot's list: one LDS atomic per wave
+                const bool nz = in && pot != 0.0;
+                const unsigned long long mask = __ballot(nz);
+                if (mask) {
+                    const int lane_id = tid & 63;
+                    const int leader = __ffsll((long long)mask) - 1;
+                    int base = 0;
+                    if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                    base = __shfl(base, leader, 64);
+                    if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(qq[u] * N + tt[u]);
+                }
+#else
+                if (in && pot != 0.0) av[qq[u] * N + tt[u]] = pot * sphere_speed(m, fb, pad, sph[sb + qq[u]], sb + qq[u], tt[u]);
+#endif
+            }
+        }
+        __syncthreads();   // pots and the non-zero list complete
+        // velocities only for the listed pairs, spread densely over the block
+#ifndef NO_COMPACT
+        for (int i = tid; i < nz_count; i += BLOCK) {
+            const int it = nzl[i];
+            const int qi = it / N, ti = it - qi * N;
+            av[it] *= sphere_speed(m, fb, pad, sph[sb + qi], sb + qi, ti);
+        }
+#endif
+        __syncthreads();   // the slot's a values complete; fb free for the next slot
+        STAMP(11 + 2 * o.slot);
+        if (t_own < N) {
+            for (int q = 0; q < se - sb; ++q) {
+                cum += av[q * N + t_own];
+                state += cum;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
         }
     }
     STAMP(4);
-}
-
-__device__ __forceinline__ void load_frame(const double* fr, int N, int tt, double* R, double* P)
-{
-#pragma unroll
-    for (int k = 0; k < 9; ++k) R[k] = fr[k * N + tt];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) P[k] = fr[(9 + k) * N + tt];
-}
-
-// One lane per (frame slot g, waypoint t): the slot's frame at t is loaded once and serves
-// every sphere of that segment; the neighbour frames needed by the velocity stencil are
-// loaded only when one of those spheres has a non-zero potential.  All loads are
-// unconditional (clamped addresses) so a lane's loads are in flight together.
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) double lds2[];
-    __shared__ int flag;
-    __shared__ int slot_sph_s[kMaxSeg + 1];
-    const int N = m.N, S = m.S, G = m.nslots;
-    const int SC = m.sph_chunk;                         // spheres per LDS chunk
-    double* av = lds2;                                  // SC*N: pot, then a = pot*|v|
-    double* pad = av + SC * N;                          // [12][S][3] padding-row positions
-    DevSphere* sph = (DevSphere*)(pad + 36 * S);        // S
-    STAMP(100);
-    const int e = blockIdx.x, tid = threadIdx.x;
-    const bool extra = e == a.num_noisy;
-    const int member = extra ? a.x_member : a.member;
-    const double* frames = a.frames + (size_t)e * G * 12 * N;
-    for (int idx = tid; idx < S; idx += BLOCK) sph[idx] = m.sph[idx];
-    for (int idx = tid; idx < 36 * S; idx += BLOCK) pad[idx] = m.pad_pos[idx];
-    for (int idx = tid; idx <= G; idx += BLOCK) slot_sph_s[idx] = m.slot_sph[idx];
-    if (tid == 0) flag = 0;
-    __syncthreads();
-
-    double cum = 0.0, state = 0.0;
-    bool col = false;
-    for (int g0 = 0; g0 < G;) {
-        // chunk of whole slots whose spheres fit in av (uniform)
-        int g1 = g0 + 1;
-        while (g1 < G && slot_sph_s[g1 + 1] - slot_sph_s[g0] <= SC) ++g1;
-        const int s0 = slot_sph_s[g0];
-        const int ns = slot_sph_s[g1] - s0;
-        const int items = (g1 - g0) * N;
-        for (int it = tid; it < items; it += BLOCK) {
-            const int g = g0 + it / N, t = it - (it / N) * N;
-            const int sb = slot_sph_s[g], se = slot_sph_s[g + 1];
-            const double* fr = frames + (size_t)g * 12 * N;
-            constexpr int NT = kVelTap1 - kVelTap0 + 1, TC = 3 - kVelTap0;   // TC: centre tap
-            double v[NT][12];
-            load_frame(fr, N, t, v[TC], v[TC] + 9);
-            bool any = false;
-            for (int q0 = sb; q0 < se; q0 += kGather) {
-                float dv[kGather];
-#pragma unroll
-                for (int k = 0; k < kGather; ++k) {
-                    const int s = min(q0 + k, se - 1);
-                    double x[3];
-                    apply(v[TC], v[TC] + 9, sph[s].pos, x);
-#ifdef PAIRS_NOGATHER
-                    dv[k] = (float)(x[0] + x[1]);
-#else
-                    dv[k] = sdf_distance(m, x);
-#endif
-                }
-#pragma unroll
-                for (int k = 0; k < kGather; ++k) {
-                    const int s = q0 + k;
-                    if (s >= se) continue;
-                    const double dd = (double)dv[k];
-                    col |= dd <= sph[s].radius;
-                    const double pot = potential(sph[s], dd);
-                    any |= pot != 0.0;
-                    av[(s - s0) * N + t] = pot;   // a = pot * |v| is +0 exactly when pot == +0
-                }
-            }
-#ifdef PAIRS_NOVEL
-            any = false;
-#endif
-            if (any) {
-                // frames at the other velocity taps t-1, t+1, t+2 (kVelTap0..kVelTap1; the
-                // remaining taps are zero, checked on the host), clamped rows
-#pragma unroll
-                for (int q = 0; q < NT; ++q) {
-                    if (q == TC) continue;
-                    const int tt = min(max(t + q - TC, 0), N - 1);
-                    load_frame(fr, N, tt, v[q], v[q] + 9);
-                }
-                for (int s = sb; s < se; ++s) {
-                    const double pot = av[(s - s0) * N + t];
-                    if (pot == 0.0) continue;
-                    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-#pragma unroll
-                    for (int q = 0; q < NT; ++q) {
-                        const double c = m.vel_coef[kVelTap0 + q];
-                        if (c == 0.0) continue;   // 0 * p adds a signed zero: |v| unchanged
-                        const int tt = t + q - TC;
-                        double y[3];
-                        if (tt >= 0 && tt < N) {
-                            apply(v[q], v[q] + 9, sph[s].pos, y);
-                        } else {
-                            const int row = tt < 0 ? tt + 6 : tt - N + 6;   // padding row 0..11
-                            const double* src = pad + (row * S + s) * 3;
-                            y[0] = src[0]; y[1] = src[1]; y[2] = src[2];
-                        }
-                        v0 += c * y[0];
-                        v1 += c * y[1];
-                        v2 += c * y[2];
-                    }
-                    av[(s - s0) * N + t] = pot * sqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                }
-            }
-        }
-        __syncthreads();
-        STAMP(102);
-        if (tid < N)
-            for (int q = 0; q < ns; ++q) {
-                cum += av[q * N + tid];
-                state += cum;
-            }
-        __syncthreads();
-        g0 = g1;
-    }
-    STAMP(103);
     if (col) flag = 1;   // every writer stores 1
-    if (tid < N) {
+    __syncthreads();     // folds done (av reused below), flag complete
+    if (t_own < N) {
         const double cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
         double* so = extra ? a.x_state : a.state_out + (long long)e * N;
-        so[tid] = cost;
-        av[tid] = cost;
+        so[t_own] = cost;
+        av[t_own] = cost;
     }
     __syncthreads();
     if (tid == 0) {
@@ -276,41 +333,73 @@ __global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a)
         double* to = extra ? a.x_total : (a.total_out ? a.total_out + e : nullptr);
         if (cfo) *cfo = cf ? 1 : 0;
         if (to) {
-            double s = av[0];
-            for (int k = 1; k < N; ++k) s += av[k];   // costs.sum() (:1155)
+            // costs.sum() (:1155), sequential; the reads are independent so they pipeline
+            double s = 0.0;
+            int k = 0;
+            for (; k + 8 <= N; k += 8) {
+                double v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = av[k + q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) s += v[q];
+            }
+            for (; k < N; ++k) s += av[k];
             *to = s;
         }
     }
-    STAMP(104);
+    STAMP(5);
+    BLOCK_END();
 }
 
 STOMP_STAMP_ACCESSORS(cost)
 
-bool cost_supported(const DevModel& m) { return m.nops <= kMaxOps && m.nseg <= kMaxSeg && m.J <= kMaxJoints; }
-
-size_t pairs_lds_bytes(int chunk, int S, int N)
+bool cost_supported(const DevModel& m)
 {
-    return (size_t)chunk * N * sizeof(double) + (size_t)S * (36 * sizeof(double) + sizeof(DevSphere));
+    return m.nops <= kMaxOps && m.nseg <= kMaxSeg && m.nslots <= kMaxSeg && m.J <= kMaxJoints && m.N <= kBlock;
 }
 
-int pairs_sphere_chunk(int S, int N)
+size_t rollout_lds_bytes(const DevModel& m, int pad_lds)
 {
-    // one double per (sphere, waypoint); chunk + sphere tables within 64 KB of LDS
-    int sc = (int)((64 * 1024 - pairs_lds_bytes(0, S, N)) / (8 * (size_t)N));
-    if (sc > S) sc = S;
-    return sc < 1 ? 1 : sc;
+    return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, pad_lds).total;
+}
+
+size_t rollout_static_lds()
+{
+    hipFuncAttributes attr;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock>) != hipSuccess) return 2048;
+    return attr.sharedSizeBytes;
+}
+
+// resident rollout workgroups per CU for a given total LDS per workgroup: the smaller of
+// the LDS limit and the register limit (4 SIMDs, 512 VGPRs per lane-slot, 8-register
+// granules; MI355X_MICROARCH.md occupancy table)
+int rollout_blocks_per_cu(size_t lds_total)
+{
+    hipFuncAttributes attr;
+    int regs = 256;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock>) == hipSuccess && attr.numRegs > 0)
+        regs = attr.numRegs;
+    const int alloc = (regs + 7) / 8 * 8;
+    int waves_per_simd = 512 / alloc;
+    if (waves_per_simd > 8) waves_per_simd = 8;
+    const int by_regs = waves_per_simd * 4 / (kBlock / 64);
+    const int by_lds = (int)(kLdsPerCu / (lds_total ? lds_total : 1));
+    return by_regs < by_lds ? by_regs : by_lds;
 }
 
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int blocks = a.num_noisy + (a.x_params ? 1 : 0);
     if (blocks <= 0) return;
-    const size_t lds1 = (size_t)m.J * m.N * 3 * sizeof(double);
-    // 256 lanes: four waves share the limited joints in handleJointLimits; the FK program
-    // runs on lanes t < N (N <= 256)
-    hipLaunchKernelGGL((k_fk<256>), dim3(blocks), dim3(256), lds1, s, m, a);
-    const size_t lds2 = pairs_lds_bytes(m.sph_chunk, m.S, m.N);
-    hipLaunchKernelGGL((k_pairs<kPairsBlock>), dim3(blocks), dim3(kPairsBlock), lds2, s, m, a);
+    const size_t lds = rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.pad_lds).total;
+    if (lds > 64 * 1024) {
+        static size_t raised = 0;   // opt in to more than the default 64 KB once per size
+        if (lds > raised) {
+            (void)hipFuncSetAttribute((const void*)k_rollout<kBlock>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            raised = lds;
+        }
+    }
+    hipLaunchKernelGGL((k_rollout<kBlock>), dim3(blocks), dim3(kBlock), lds, s, m, a);
 }
 
 }  // namespace stomp

@@ -20,7 +20,7 @@ namespace stomp {
 constexpr int kMaxJoints = 32;
 constexpr int kRunMaxSmall = 12;  // spheres per FK op when N <= 128 (LDS batch)
 constexpr int kRunMaxLarge = 8;   // spheres per FK op when N > 128
-constexpr int kSaves = 2;         // saved branch-point FK frames per thread (registers)
+constexpr int kSaves = 2;         // saved branch-point FK frames (LDS, one column per waypoint)
 constexpr int kSumBlock = 64;     // canonical blocked summation over rollouts
 constexpr int kVelTap0 = 2;       // non-zero taps of the velocity rule DIFF_RULES[0]
 constexpr int kVelTap1 = 5;       // (stomp_utils.h:54), checked in stomp_engine_create
@@ -54,7 +54,9 @@ struct FkOp {
 };
 
 struct DevModel {
-    int J, N, Nall, S, nops, nseg, nslots, sph_chunk;
+    int J, N, Nall, S, nops, nseg, nslots, sph_chunk;   // sph_chunk: most spheres on one segment
+    int nsaves;                 // saved branch-point frames the FK program uses (0..kSaves, LDS)
+    int pad_lds;                // padding-row positions staged in LDS (1) or read from HBM (0)
     const DevSegment* segs;
     const DevSphere* sph;
     const FkOp* ops;
@@ -99,7 +101,6 @@ struct NoiseArgs {
 // Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
 // x_params) evaluates the noiseless rollout of theta (pipelined from the previous iteration).
 struct CostArgs {
-    double* frames;             // [blocks][nslots][12][N] scratch between k_fk and k_pairs
     const double* params;
     long long stride;
     int num_noisy;
@@ -135,8 +136,14 @@ struct WeightArgs {
 void launch_noise(const NoiseArgs& a, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);
-int pairs_sphere_chunk(int S, int N);
-size_t pairs_lds_bytes(int chunk, int S, int N);
+size_t rollout_lds_bytes(const DevModel& m, int pad_lds);   // dynamic LDS of the rollout kernel
+size_t rollout_static_lds();                                 // its static LDS
+int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS and register limits)
+// LDS per CU is 160 KiB (MI355X_MICROARCH.md), but three 49.5 KB rollout workgroups did not
+// co-reside on one CU in our residency measurements (tools/stamps.py) while three 46.9 KB
+// ones did, so the occupancy model budgets 144 KiB
+constexpr size_t kLdsPerCu = 144 * 1024;
+constexpr size_t kRolloutLdsMax = 156 * 1024;                // dynamic + static per workgroup
 void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
 void launch_weights(const WeightArgs& a, hipStream_t s);
 int weights_tile(int K_loc);

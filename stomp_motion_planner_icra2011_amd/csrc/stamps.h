@@ -20,6 +20,27 @@ static __device__ int g_stamp_block;
         }                                                                                               \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
+// Per-workgroup residency record: {HW_ID, XCC_ID, start, end} for blocks < 8192, to measure
+// how many workgroups of a launch actually share a CU.
+static __device__ unsigned long long g_blocks[8192][4];
+#define BLOCK_BEGIN()                                                                                   \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                    \
+            unsigned long long _t;                                                                      \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
+            g_blocks[blockIdx.x][0] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);             \
+            g_blocks[blockIdx.x][1] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);            \
+            g_blocks[blockIdx.x][2] = _t;                                                               \
+        }                                                                                               \
+    } while (0)
+#define BLOCK_END()                                                                                     \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                    \
+            unsigned long long _t;                                                                      \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
+            g_blocks[blockIdx.x][3] = _t;                                                               \
+        }                                                                                               \
+    } while (0)
 #define STOMP_STAMP_ACCESSORS(name)                                                                     \
     extern "C" int stomp_debug_stamps_##name(int block, unsigned long long* out, int reset)            \
     {                                                                                                   \
@@ -30,10 +51,20 @@ static __device__ int g_stamp_block;
             hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_block), &block, sizeof(int));                          \
         }                                                                                               \
         return 0;                                                                                       \
+    }                                                                                                   \
+    extern "C" int stomp_debug_blocks_##name(unsigned long long* out)                                  \
+    {                                                                                                   \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blocks), sizeof(g_blocks)) == hipSuccess ? 0 : -1; \
     }
 #else
 #define STAMP(i) \
     do {         \
+    } while (0)
+#define BLOCK_BEGIN() \
+    do {              \
+    } while (0)
+#define BLOCK_END() \
+    do {            \
     } while (0)
 #define STOMP_STAMP_ACCESSORS(name)
 #endif

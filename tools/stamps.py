@@ -47,12 +47,47 @@ def show(name, block, labels):
 
 
 def cost_label(i):
-    return {0: "fk: start", 1: "fk: tables loaded", 2: "fk: joint limits", 3: "fk: sincos", 4: "fk: frames",
-            100: "pairs: start", 101: "pairs: pos+gather", 102: "pairs: pot+vel", 103: "pairs: fold",
-            104: "pairs: end"}.get(i, str(i))
+    if 10 <= i < 100:
+        g = (i - 10) // 2
+        return f"slot {g}: " + ("FK + fold + publish" if i % 2 == 0 else "pairs")
+    return {0: "start", 1: "tables loaded", 2: "joint limits", 3: "sincos", 4: "FK/pairs done",
+            5: "end"}.get(i, str(i))
 
 
 show("cost", 0, cost_label)
 show("cost", K, cost_label)   # the pipelined noiseless rollout
 show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
 show("weights", 0, lambda i: ["start", "load+minmax", "exp", "psum", "u partials", "end"][i])
+
+
+def residency():
+    """Workgroups of one rollout-cost launch per CU, and their overlap in time."""
+    fn = lib.stomp_debug_blocks_cost
+    fn.argtypes = [C.c_void_p]
+    buf = np.zeros((8192, 4), np.uint64)
+    e.run(7, 1)
+    e.synchronize()
+    fn(buf.ctypes.data)
+    b = buf[: K + 1].astype(np.int64)
+    cu = ((b[:, 1] & 0xF) << 8) | ((b[:, 0] >> 8) & 0xFF)
+    t0, t1 = b[:, 2], b[:, 3]
+    import collections
+    per = collections.defaultdict(list)
+    for i in range(len(b)):
+        per[int(cu[i])].append((int(t0[i]), int(t1[i])))
+    conc = []
+    for v in per.values():
+        ev = sorted([(a, 1) for a, _ in v] + [(c, -1) for _, c in v])
+        cur = mx = 0
+        for _, d in ev:
+            cur += d
+            mx = max(mx, cur)
+        conc.append(mx)
+    span = int(t1.max() - t0.min())
+    print(f"--- residency: {len(per)} CUs used by {len(b)} workgroups; per CU: "
+          f"{collections.Counter(len(v) for v in per.values())}; max concurrent per CU: {collections.Counter(conc)}")
+    print(f"    launch span {span} cycles; workgroup duration min/median/max "
+          f"{int((t1 - t0).min())}/{int(np.median(t1 - t0))}/{int((t1 - t0).max())}")
+
+
+residency()
