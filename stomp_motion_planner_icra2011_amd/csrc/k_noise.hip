@@ -193,12 +193,15 @@ void launch_noise(const NoiseArgs& a, hipStream_t s)
     const int rows = a.K_loc - a.row_begin;
     if (rows <= 0) return;
     const int block = a.N <= 128 ? 128 : 256;
-    const int rt = rows >= 8 ? 8 : 1;
+#ifndef NOISE_RT
+#define NOISE_RT 4
+#endif
+    const int rt = rows >= NOISE_RT ? NOISE_RT : 1;
     const size_t lds = (size_t)rt * (2 * a.N + 2 * a.Nall) * sizeof(double);
     dim3 grid((rows + rt - 1) / rt, a.J);
-    if (rt == 8) {
-        if (block == 128) hipLaunchKernelGGL((k_noise<128, 8>), grid, dim3(128), lds, s, a);
-        else hipLaunchKernelGGL((k_noise<256, 8>), grid, dim3(256), lds, s, a);
+    if (rt == NOISE_RT) {
+        if (block == 128) hipLaunchKernelGGL((k_noise<128, NOISE_RT>), grid, dim3(128), lds, s, a);
+        else hipLaunchKernelGGL((k_noise<256, NOISE_RT>), grid, dim3(256), lds, s, a);
     } else {
         if (block == 128) hipLaunchKernelGGL((k_noise<128, 1>), grid, dim3(128), lds, s, a);
         else hipLaunchKernelGGL((k_noise<256, 1>), grid, dim3(256), lds, s, a);
