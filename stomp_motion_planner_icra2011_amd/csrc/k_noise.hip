@@ -19,28 +19,44 @@
 
 namespace stomp {
 
-// acc[rr] += sum_{k < kend} AT[k][i] * v[k][rr], k ascending.  Unconditional clamped loads,
-// double-buffered: the next eight AT values are in flight while the current eight are used.
+// acc[rr] += sum_{k < kend} AT[k][i] * v[k][rr], k ascending.  Unconditional clamped loads in
+// four 8-load batches that rotate roles without register copies, so three batches are in
+// flight while one is summed (a copy of the next batch into the current one would make
+// the compiler wait for the batch it has just issued).
 template <int RT>
 __device__ __forceinline__ void band_product(const double* __restrict__ AT, int N, int i, int kend,
                                              const double* v, double* acc)
 {
-    double cur[8];
+    constexpr int P = 8;
+    double A0[P], A1[P], A2[P], A3[P];
+    auto load = [&](double* buf, int k0) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) cur[q] = AT[(size_t)min(q, N - 1) * N + i];
-    for (int k0 = 0; k0 < kend; k0 += 8) {
-        double nxt[8];
+        for (int q = 0; q < P; ++q) buf[q] = AT[(size_t)min(k0 + q, N - 1) * N + i];
+    };
+    auto sum = [&](const double* buf, int k0) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = AT[(size_t)min(k0 + 8 + q, N - 1) * N + i];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const double c = k0 + q < N ? cur[q] : 0.0;
+        for (int q = 0; q < P; ++q) {
+            const double c = k0 + q < N ? buf[q] : 0.0;
             const double* x = v + min(k0 + q, N - 1) * RT;
 #pragma unroll
             for (int rr = 0; rr < RT; ++rr) acc[rr] += c * x[rr];
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    };
+    load(A0, 0);
+    load(A1, P);
+    load(A2, 2 * P);
+    for (int k0 = 0; k0 < kend; k0 += 4 * P) {
+        load(A3, k0 + 3 * P);
+        sum(A0, k0);
+        if (k0 + P >= kend) break;
+        load(A0, k0 + 4 * P);
+        sum(A1, k0 + P);
+        if (k0 + 2 * P >= kend) break;
+        load(A1, k0 + 5 * P);
+        sum(A2, k0 + 2 * P);
+        if (k0 + 3 * P >= kend) break;
+        load(A2, k0 + 6 * P);
+        sum(A3, k0 + 3 * P);
     }
 }
 

@@ -242,21 +242,35 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
     }
     __syncthreads();
     if (i >= N) return;
-    // k ascending; clamped unconditional loads, the next 16 in flight while 16 are summed
+    // k ascending; four 16-load batches rotate (no register copies), so three are in flight
+    // while one is summed
     constexpr int B = 16;
     double s = 0.0;
-    double cur[B];
+    double A0[B], A1[B], A2[B], A3[B];
+    auto load = [&](double* buf, int k0) {
 #pragma unroll
-    for (int q = 0; q < B; ++q) cur[q] = MT[(size_t)min(q, N - 1) * N + i];
-    for (int k0 = 0; k0 < N; k0 += B) {
-        double nxt[B];
-#pragma unroll
-        for (int q = 0; q < B; ++q) nxt[q] = MT[(size_t)min(k0 + B + q, N - 1) * N + i];
+        for (int q = 0; q < B; ++q) buf[q] = MT[(size_t)min(k0 + q, N - 1) * N + i];
+    };
+    auto sum = [&](const double* buf, int k0) {
 #pragma unroll
         for (int q = 0; q < B; ++q)
-            if (k0 + q < N) s += cur[q] * us[k0 + q];
-#pragma unroll
-        for (int q = 0; q < B; ++q) cur[q] = nxt[q];
+            if (k0 + q < N) s += buf[q] * us[k0 + q];
+    };
+    load(A0, 0);
+    load(A1, B);
+    load(A2, 2 * B);
+    for (int k0 = 0; k0 < N; k0 += 4 * B) {
+        load(A3, k0 + 3 * B);
+        sum(A0, k0);
+        if (k0 + B >= N) break;
+        load(A0, k0 + 4 * B);
+        sum(A1, k0 + B);
+        if (k0 + 2 * B >= N) break;
+        load(A1, k0 + 5 * B);
+        sum(A2, k0 + 2 * B);
+        if (k0 + 3 * B >= N) break;
+        load(A2, k0 + 6 * B);
+        sum(A3, k0 + 3 * B);
     }
     theta[(size_t)d * N + i] += 1.0 * s;
 }
