@@ -307,9 +307,18 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(11 + 2 * o.slot);
         if (t_own < N) {
-            for (int q = 0; q < se - sb; ++q) {
-                cum += av[q * N + t_own];
-                state += cum;
+            // fold in sphere order; the LDS reads go out 16 at a time
+            const int nsl = se - sb;
+            for (int q0 = 0; q0 < nsl; q0 += 16) {
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, nsl - 1) * N + t_own];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (q0 + q >= nsl) break;
+                    cum += v[q];
+                    state += cum;
+                }
             }
 #pragma unroll
             for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];

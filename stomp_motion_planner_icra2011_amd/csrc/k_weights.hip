@@ -17,6 +17,22 @@
 
 namespace stomp {
 
+// sum_{q < count} p[q * stride], q ascending from 0.0; the LDS reads go out 16 at a time so
+// the chain waits on one LDS latency per 16 terms instead of one per term
+__device__ __forceinline__ double lds_seq_sum(const double* p, int stride, int count)
+{
+    double s = 0.0;
+    for (int q0 = 0; q0 < count; q0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = p[min(q0 + q, count - 1) * stride];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q0 + q < count) s += v[q];
+    }
+    return s;
+}
+
 // EPT: cost-tile elements per lane, K_loc * TC <= EPT * 256
 template <int EPT>
 __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
@@ -84,9 +100,19 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
             __syncthreads();
             if (tid < TC) {
                 double mn = red0[tid], mx = red1[tid];
-                for (int j = tid + TC; j < BLOCK; j += TC) {
-                    if (red0[j] < mn) mn = red0[j];
-                    if (red1[j] > mx) mx = red1[j];
+                for (int j0 = tid + TC; j0 < BLOCK; j0 += 16 * TC) {
+                    double x0[16], x1[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int j = min(j0 + q * TC, BLOCK - TC + tid);   // stays in this column
+                        x0[q] = red0[j];
+                        x1[q] = red1[j];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {   // order-free; the clamped repeats are harmless
+                        if (x0[q] < mn) mn = x0[q];
+                        if (x1[q] > mx) mx = x1[q];
+                    }
                 }
                 red0[tid] = mn;   // only lanes < TC read these slots from here on
                 red1[tid] = mx;
@@ -112,8 +138,7 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
         if (tid < nb * TC) {
             const int b = tid / TC, cc = tid % TC;
             const int r1 = min(K, (b + 1) * kSumBlock);
-            double s = 0.0;
-            for (int r = b * kSumBlock; r < r1; ++r) s += V[r * TC + cc];
+            const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TC + cc, TC, r1 - b * kSumBlock);
             part[tid] = s;
             if (a.mode == W_PSUM && t0 + cc < N) a.psum_part[(size_t)b * JN + (size_t)d * N + t0 + cc] = s;
         }
@@ -165,8 +190,7 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
     if (tid < nb * TC) {
         const int b = tid / TC, cc = tid % TC;
         const int r1 = min(K, (b + 1) * kSumBlock);
-        double s = 0.0;
-        for (int r = b * kSumBlock; r < r1; ++r) s += V[r * TC + cc];
+        const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TC + cc, TC, r1 - b * kSumBlock);
         part[tid] = s;
         if (a.mode == W_USUM && t0 + cc < N) a.u_part[(size_t)b * JN + (size_t)d * N + t0 + cc] = s;
     }
@@ -185,10 +209,13 @@ STOMP_STAMP_ACCESSORS(weights)
 
 // columns per workgroup: as many as keep K_loc * TC <= 2048 (more workgroups, shorter
 // per-lane chains); K_loc in (2048, 4096] runs one column per workgroup with EPT = 16
+#ifndef WEIGHTS_TILE_ELEMS
+#define WEIGHTS_TILE_ELEMS 2048
+#endif
 int weights_tile(int K_loc)
 {
     int tc = 16;
-    while (tc > 1 && (size_t)K_loc * tc > 2048) tc >>= 1;
+    while (tc > 1 && (size_t)K_loc * tc > WEIGHTS_TILE_ELEMS) tc >>= 1;
     return tc;
 }
 
@@ -196,7 +223,7 @@ void launch_weights(const WeightArgs& a, hipStream_t s)
 {
     dim3 grid((a.N + a.tc - 1) / a.tc, a.J);
     const size_t lds = (size_t)a.K_loc * a.tc * sizeof(double);
-    if ((size_t)a.K_loc * a.tc <= 2048)
+    if ((size_t)a.K_loc * a.tc <= 2048 && WEIGHTS_TILE_ELEMS <= 2048)
         hipLaunchKernelGGL((k_weights<8>), grid, dim3(256), lds, s, a);
     else
         hipLaunchKernelGGL((k_weights<16>), grid, dim3(256), lds, s, a);
