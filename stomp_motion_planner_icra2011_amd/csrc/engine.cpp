@@ -492,7 +492,9 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (!msg.empty()) CREATE_TRY(fail(e, STOMP_E_INVALID, "%s", msg.c_str()));
 
     const int J = e->J, N = e->N;
-    std::vector<double> LT((size_t)N * N), MT((size_t)N * N), QT((size_t)J * N * N);
+    // LT / MT carry kMatPadRows zero rows past N for the noise kernel's unclamped look-ahead loads
+    std::vector<double> LT((size_t)(N + kMatPadRows) * N, 0.0), MT((size_t)(N + kMatPadRows) * N, 0.0),
+        QT((size_t)J * N * N);
     for (int i = 0; i < N; ++i)
         for (int k = 0; k < N; ++k) {
             LT[(size_t)k * N + i] = e->su.L[(size_t)i * N + k];

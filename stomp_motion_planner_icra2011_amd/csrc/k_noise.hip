@@ -27,19 +27,21 @@ template <int RT>
 __device__ __forceinline__ void band_product(const double* __restrict__ AT, int N, int i, int kend,
                                              const double* v, double* acc)
 {
-    constexpr int P = 8;
+    // AT has kMatPadRows zero rows past N and v (LDS) kBandPad zero rows past N, so neither the
+    // loads nor the sums need clamping: terms past kend are exact no-ops (zeros of L^T above
+    // the diagonal or of the padding; the accumulator is never -0.0, see the caller)
+    constexpr int P = kBandBatch;
     double A0[P], A1[P], A2[P], A3[P];
     auto load = [&](double* buf, int k0) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) buf[q] = AT[(size_t)min(k0 + q, N - 1) * N + i];
+        for (int q = 0; q < P; ++q) buf[q] = AT[(size_t)(k0 + q) * N + i];
     };
     auto sum = [&](const double* buf, int k0) {
 #pragma unroll
         for (int q = 0; q < P; ++q) {
-            const double c = k0 + q < N ? buf[q] : 0.0;
-            const double* x = v + min(k0 + q, N - 1) * RT;
+            const double* x = v + (k0 + q) * RT;
 #pragma unroll
-            for (int rr = 0; rr < RT; ++rr) acc[rr] += c * x[rr];
+            for (int rr = 0; rr < RT; ++rr) acc[rr] += buf[q] * x[rr];
         }
     };
     load(A0, 0);
@@ -65,9 +67,10 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int N = a.N, Nall = a.Nall, J = a.J;
-    double* zs = lds;              // N*RT   [k][rr]
-    double* eps = zs + RT * N;     // N*RT   [k][rr]
-    double* xs = eps + RT * N;     // RT*Nall
+    const int NB = N + kBandBatch;   // rows incl. the zero padding the band products read
+    double* zs = lds;              // NB*RT  [k][rr]
+    double* eps = zs + RT * NB;    // NB*RT  [k][rr]
+    double* xs = eps + RT * NB;    // RT*Nall
     double* cs = xs + RT * Nall;   // RT*Nall
     const int d = blockIdx.y;
     const int r0 = a.row_begin + blockIdx.x * RT;
@@ -76,6 +79,10 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     const double sig = a.sigma.v[d];
     STAMP(0);
 
+    for (int idx = tid; idx < kBandBatch * RT; idx += BLOCK) {
+        zs[N * RT + idx] = 0.0;
+        eps[N * RT + idx] = 0.0;
+    }
     bool gen[RT];
     bool any_gen = false;
 #pragma unroll
@@ -163,17 +170,22 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     __syncthreads();
 
     for (int ii = tid; ii < Nall; ii += BLOCK) {
-        const int c0 = ii - 3 < 0 ? 0 : ii - 3;
-        const int c1 = ii + 3 >= Nall ? Nall - 1 : ii + 3;
+        // the 7-tap window of every rollout first (all LDS reads in flight), then the sums over
+        // the taps inside [0, Nall) in ascending order
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
+            double xw[7];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) xw[q] = xs[rr * Nall + min(max(ii - 3 + q, 0), Nall - 1)];
             double call = 0.0;
 #pragma unroll
             for (int rule = 0; rule < 3; ++rule) {
                 const double wr = a.wr[rule];
                 if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
                 double s = 0.0;
-                for (int c = c0; c <= c1; ++c) s += a.dcoef[rule][c - ii + 3] * xs[rr * Nall + c];
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (ii - 3 + q >= 0 && ii - 3 + q < Nall) s += a.dcoef[rule][q] * xw[q];
                 call += wr * (s * s);
             }
             cs[rr * Nall + ii] = call;
@@ -213,7 +225,7 @@ void launch_noise(const NoiseArgs& a, hipStream_t s)
 #define NOISE_RT 4
 #endif
     const int rt = rows >= NOISE_RT ? NOISE_RT : 1;
-    const size_t lds = (size_t)rt * (2 * a.N + 2 * a.Nall) * sizeof(double);
+    const size_t lds = (size_t)rt * (2 * (a.N + kBandBatch) + 2 * a.Nall) * sizeof(double);
     dim3 grid((rows + rt - 1) / rt, a.J);
     if (rt == NOISE_RT) {
         if (block == 128) hipLaunchKernelGGL((k_noise<128, NOISE_RT>), grid, dim3(128), lds, s, a);
