@@ -244,7 +244,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
         if (tid == 0) nz_count = 0;
         __syncthreads();   // frame published; every lane's previous fold is done
-        STAMP(10 + 2 * o.slot);
+        STAMP(10 + 4 * o.slot);
         const int sb = slot_sph_s[o.slot], se = slot_sph_s[o.slot + 1];
         // lane = consecutive (sphere, waypoint) pairs of the slot, kPairUnroll in flight
         // lane takes pairs (q, t) = (tid / N, tid % N) + k * BLOCK, stepped without dividing
@@ -296,6 +296,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
             }
         }
         __syncthreads();   // pots and the non-zero list complete
+        STAMP(11 + 4 * o.slot);
         // velocities only for the listed pairs, spread densely over the block
 #ifndef NO_COMPACT
         for (int i = tid; i < nz_count; i += BLOCK) {
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
 #endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
-        STAMP(11 + 2 * o.slot);
+        STAMP(12 + 4 * o.slot);
         if (t_own < N) {
             // fold in sphere order; the LDS reads go out 16 at a time
             const int nsl = se - sb;
@@ -325,6 +326,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 #pragma unroll
             for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
         }
+        STAMP(13 + 4 * o.slot);
     }
     STAMP(4);
     if (col) flag = 1;   // every writer stores 1

@@ -48,8 +48,8 @@ def show(name, block, labels):
 
 def cost_label(i):
     if 10 <= i < 100:
-        g = (i - 10) // 2
-        return f"slot {g}: " + ("FK + fold + publish" if i % 2 == 0 else "pairs")
+        g, ph = (i - 10) // 4, (i - 10) % 4
+        return f"slot {g}: " + ["FK + publish", "positions+gathers+pots", "velocity", "fold (lanes t<N)"][ph]
     return {0: "start", 1: "tables loaded", 2: "joint limits", 3: "sincos", 4: "FK/pairs done",
             5: "end"}.get(i, str(i))
 
