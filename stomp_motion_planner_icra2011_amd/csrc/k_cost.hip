@@ -51,23 +51,28 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
                                                const DevSphere& sp, int s, int t)
 {
     const int N = m.N;
+    // every tap's free-row position and padding-row position are fetched unconditionally
+    // (clamped indices, all reads in flight together) and the right one selected per tap
+    double y[7][3];
+#pragma unroll
+    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
+        const int tt = t + kk - 3;
+        double yf[3];
+        apply_lds(fb, N, min(max(tt, 0), N - 1), sp.pos, yf);
+        const int row = tt < 0 ? tt + 6 : (tt >= N ? tt - N + 6 : 0);   // padding row 0..11
+        const double* src = pad + (row * m.S + s) * 3;
+        const bool in = tt >= 0 && tt < N;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) y[kk][c] = in ? yf[c] : src[c];
+    }
     double v0 = 0.0, v1 = 0.0, v2 = 0.0;
 #pragma unroll
     for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
         const double c = m.vel_coef[kk];
         if (c == 0.0) continue;   // 0 * p adds a signed zero: |v| unchanged
-        const int tt = t + kk - 3;
-        double y[3];
-        if (tt >= 0 && tt < N) {
-            apply_lds(fb, N, tt, sp.pos, y);
-        } else {
-            const int row = tt < 0 ? tt + 6 : tt - N + 6;   // padding row 0..11
-            const double* src = pad + (row * m.S + s) * 3;
-            y[0] = src[0]; y[1] = src[1]; y[2] = src[2];
-        }
-        v0 += c * y[0];
-        v1 += c * y[1];
-        v2 += c * y[2];
+        v0 += c * y[kk][0];
+        v1 += c * y[kk][1];
+        v2 += c * y[kk][2];
     }
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
 }
