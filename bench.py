@@ -11,9 +11,10 @@ the K dimension is sharded (K = 512 N, weak scaling) and the per-iteration
 reductions run over RCCL inside the engine.
 
 Also reported:
-  roofline      dominant stage (rollout_cost = k_fk + k_pairs, Task::execute): algorithmic bytes
-                per launch (K_loc + 1) * N * (4 S + 8 J + 8) over its HIP-event duration, from a
-                second pass of the same K steps with events (the value pass has none)
+  roofline      dominant stage (rollout_cost = fused k_rollout: noise generation + Task::execute):
+                algorithmic bytes per launch K_loc N (4 S + 24 J + 8) + N (4 S + 8 J + 8) over its
+                HIP-event duration, from a second pass of the same K steps with events (the value
+                pass has none)
   cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread)
                 timed on this host on a bounded sample of the same workload
 """
@@ -141,15 +142,17 @@ def main():
 
     S = len(p.spheres)
     K_loc = e.K_loc
-    # each launch evaluates K_loc noisy rollouts + the deferred noiseless rollout of theta
-    bytes_per_launch = (K_loc + 1) * p.N * (4 * S + 8 * p.J + 8)
+    # each launch generates and evaluates K_loc noisy rollouts (noise, params and control rows
+    # written: 24 J N bytes; SDF gathers 4 S N; state costs 8 N) and evaluates the deferred
+    # noiseless rollout of theta (reads 8 J N)
+    bytes_per_launch = K_loc * p.N * (4 * S + 24 * p.J + 8) + p.N * (4 * S + 8 * p.J + 8)
     roofline = None
     if timing.get("rollout_cost", {}).get("launches"):
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
         achieved = bytes_per_launch / avg_s / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": latest_traffic(),
-                    "kernel": "rollout_cost (k_fk + k_pairs)", "bytes_per_launch": bytes_per_launch,
+                    "kernel": "rollout_cost (k_rollout)", "bytes_per_launch": bytes_per_launch,
                     "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3)}
     if roofline is not None:
         # whole iteration, B_iter = E * N * (4 S + 16 J + 8), E = K + 1, all ranks

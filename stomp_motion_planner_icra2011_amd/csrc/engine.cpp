@@ -319,15 +319,26 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         e->extra_added = false;
     }
     na.K_gen_global = e->K_gen;
-    {
+    // generated rows [0, g1 - g0) of this shard: their noise is made by the rollout kernel
+    // itself (fused), k_noise only projects and prices the reused rows after them
+    const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
+    const int num_gen = std::max(g1 - g0, 0);
+#ifndef STOMP_SEPARATE_NOISE
+    const bool fused = e->N <= 128;   // rollout_project's register tiling covers 128 waypoints
+#else
+    const bool fused = false;
+#endif
+    if (fused) na.row_begin = num_gen;
+    if (na.row_begin < na.K_loc) {
         Timed tm(e, T_NOISE);
         launch_noise(na, e->stream);
     }
     // Task::execute for the generated rollouts of this shard (+ the pending noiseless rollout)
     {
-        const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
         CostArgs ca{};
-            ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = std::max(g1 - g0, 0);
+        ca.fused_noise = fused ? 1 : 0;
+        ca.nz = na;
+        ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
@@ -530,14 +541,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     // slots are numbered in sphere order, so each slot owns a contiguous sphere range
     std::vector<int> slot_sph(e->nslots + 1, e->S);
     for (int j = e->S - 1; j >= 0; --j) slot_sph[e->sphere_slot[j]] = j;
-    DevSegment* d_segs; DevSphere* d_sph; FkOp* d_ops; int* d_hl; int* d_slot_sph; double *d_jmin, *d_jmax;
-    CREATE_TRY(upload(e, &d_slot_sph, slot_sph.data(), slot_sph.size()));
-    CREATE_TRY(upload(e, &d_segs, segs.data(), segs.size()));
-    CREATE_TRY(upload(e, &d_sph, sph.data(), sph.size()));
-    CREATE_TRY(upload(e, &d_ops, e->ops.data(), e->ops.size()));
-    CREATE_TRY(upload(e, &d_hl, has_lim.data(), has_lim.size()));
-    CREATE_TRY(upload(e, &d_jmin, jmin.data(), jmin.size()));
-    CREATE_TRY(upload(e, &d_jmax, jmax.data(), jmax.size()));
     CREATE_TRY(upload(e, &e->d_QT, QT.data(), QT.size()));
     CREATE_TRY(upload(e, &e->d_LT, LT.data(), LT.size()));
     CREATE_TRY(upload(e, &e->d_MT, MT.data(), MT.size()));
@@ -576,7 +579,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_cf, 1));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
-    CREATE_TRY(dev_alloc(e, &e->d_pad_pos, (size_t)12 * std::max(e->S, 1) * 3));
     CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
     if (hipHostMalloc((void**)&e->h_total, sizeof(double)) != hipSuccess ||
         hipHostMalloc((void**)&e->h_cf, 16) != hipSuccess)
@@ -606,7 +608,35 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     if (!cost_supported(m)) CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "FK program too large (%d ops, %d segments)",
                                             m.nops, m.nseg));
-    m.segs = d_segs; m.sph = d_sph; m.ops = d_ops; m.slot_sph = d_slot_sph; m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
+    {
+        // the rollout kernel's LDS table image (RolloutLds from .sph on), padding positions last
+        const RolloutLds L = rollout_lds(J, N, e->S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, 1);
+        std::vector<unsigned char> img(L.total - L.sph, 0);
+        auto put = [&](size_t off, const void* src, size_t bytes) {
+            if (bytes) std::memcpy(img.data() + (off - L.sph), src, bytes);
+        };
+        std::vector<double> jlim(2 * (size_t)J);
+        for (int j = 0; j < J; ++j) { jlim[2 * j] = jmin[j]; jlim[2 * j + 1] = jmax[j]; }
+        put(L.sph, sph.data(), sizeof(DevSphere) * e->S);
+        put(L.seg, segs.data(), sizeof(DevSegment) * segs.size());
+        put(L.ops, e->ops.data(), sizeof(FkOp) * e->ops.size());
+        put(L.slot, slot_sph.data(), sizeof(int) * slot_sph.size());
+        put(L.hl, has_lim.data(), sizeof(int) * J);
+        put(L.jlim, jlim.data(), sizeof(double) * jlim.size());
+        unsigned long long* d_img;
+        CREATE_TRY(upload(e, &d_img, (const unsigned long long*)img.data(), img.size() / 8));
+        if (hipStreamSynchronize(e->stream) != hipSuccess)   // img is pageable and goes out of scope
+            CREATE_TRY(fail(e, STOMP_E_DEVICE, "table upload failed"));
+        const unsigned char* base = (const unsigned char*)d_img;
+        m.img = d_img;
+        m.img_words = (int)(((m.pad_lds ? L.total : L.pad) - L.sph) / 8);
+        m.sph = (const DevSphere*)(base + (L.sph - L.sph));
+        m.segs = (const DevSegment*)(base + (L.seg - L.sph));
+        m.ops = (const FkOp*)(base + (L.ops - L.sph));
+        m.slot_sph = (const int*)(base + (L.slot - L.sph));
+        e->d_pad_pos = (double*)(base + (L.pad - L.sph));
+    }
+    m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
     m.inv_res = 1.0 / d->grid.resolution;
@@ -618,7 +648,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "velocity rule tap %d outside the kernel's stencil", k));
     }
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
-    m.has_limits = d_hl; m.jmin = d_jmin; m.jmax = d_jmax; m.QT = e->d_QT;
+    m.QT = e->d_QT;
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
     int pad_cf = 0;

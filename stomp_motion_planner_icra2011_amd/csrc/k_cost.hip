@@ -20,6 +20,7 @@
 // The extra workgroup (index num_noisy) evaluates the noiseless rollout of theta that the
 // previous iteration deferred (policy_improvement_loop.cpp:180-182).
 #include "device_fk.h"
+#include "noise_device.h"
 #include "stamps.h"
 
 namespace stomp {
@@ -34,7 +35,8 @@ constexpr int kBlock = 256;
 #ifndef PAIR_UNROLL
 #define PAIR_UNROLL 4
 #endif
-constexpr int kPairUnroll = PAIR_UNROLL;   // spheres per lane with gathers in flight   // (sphere, waypoint) pairs per lane in flight
+constexpr int kPairUnroll = PAIR_UNROLL;   // (sphere, waypoint) pairs per lane in flight
+constexpr int kCopyBatch = 12;             // table-image words per lane per copy pass
 }
 
 __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
@@ -77,52 +79,25 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
 }
 
-// LDS carve-up (bytes), shared with the host-side size check
-struct RolloutLds {
-    size_t sc, traj, fb, sv, av, nzl, sph, seg, ops, pad, total;
-};
-
-__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-// traj stays resident (the FK lanes take sin/cos of their own joint values as they go);
-// the per-slot buffers follow it
-__host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_slot, int nsaves, int nseg, int nops,
-                                                  int pad_lds)
-{
-    RolloutLds l;
-    l.sc = 0;   // unused: no sin/cos table
-    l.traj = 0;
-    l.fb = l.traj + (size_t)J * N * sizeof(double);
-    l.sv = l.fb + (size_t)12 * N * sizeof(double);
-    l.av = l.sv + (size_t)nsaves * 12 * N * sizeof(double);
-    l.nzl = l.av + (size_t)max_slot * N * sizeof(double);
-    l.sph = align16(l.nzl + (size_t)max_slot * N * sizeof(unsigned short));
-    l.seg = align16(l.sph + (size_t)S * sizeof(DevSphere));
-    l.ops = align16(l.seg + (size_t)nseg * sizeof(DevSegment));
-    l.pad = align16(l.ops + (size_t)nops * sizeof(FkOp));
-    l.total = l.pad + (pad_lds ? (size_t)36 * S * sizeof(double) : 0);
-    return l;
-}
-
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    __shared__ int slot_sph_s[kMaxSeg + 1];
-    __shared__ double jlim_s[2 * kMaxJoints];
-    __shared__ int hl_s[kMaxJoints];
     __shared__ int flag;
     __shared__ int nz_count;
     const int J = m.J, N = m.N, S = m.S;
-    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.pad_lds);
+    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
     double* traj = (double*)(lds_raw + L.traj);   // J*N
     double* fb = (double*)(lds_raw + L.fb);       // 12*N frame of the current slot
     double* sv = (double*)(lds_raw + L.sv);       // nsaves*12*N saved branch-point frames
-    double* av = (double*)(lds_raw + L.av);
-    unsigned short* nzl = (unsigned short*)(lds_raw + L.nzl);   // pairs q*N+t with a non-zero potential       // max_slot*N: pot, then pot * |v|
-    DevSphere* sph = (DevSphere*)(lds_raw + L.sph);
-    DevSegment* seg_s = (DevSegment*)(lds_raw + L.seg);
-    FkOp* ops_s = (FkOp*)(lds_raw + L.ops);
+    double* av = (double*)(lds_raw + L.av);       // max_slot*N: pot, then pot * |v|
+    unsigned short* nzl = (unsigned short*)(lds_raw + L.nzl);   // pairs q*N+t with a non-zero potential
+    const DevSphere* sph = (const DevSphere*)(lds_raw + L.sph);
+    const DevSegment* seg_s = (const DevSegment*)(lds_raw + L.seg);
+    const FkOp* ops_s = (const FkOp*)(lds_raw + L.ops);
+    const int* slot_sph_s = (const int*)(lds_raw + L.slot);
+    const int* hl_s = (const int*)(lds_raw + L.hl);
+    const double* jlim_s = (const double*)(lds_raw + L.jlim);
     // [12][S][3] padding-row sphere positions: LDS copy when it fits, else HBM
     const double* pad = m.pad_lds ? (const double*)(lds_raw + L.pad) : m.pad_pos;
 
@@ -132,19 +107,37 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     constexpr int NW = BLOCK / 64;
     const bool extra = e == a.num_noisy;
     const int member = extra ? a.x_member : a.member;
-    const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
-    for (int idx = tid; idx < J * N; idx += BLOCK) traj[idx] = prm[idx];
-    for (int idx = tid; idx < m.nops; idx += BLOCK) ops_s[idx] = m.ops[idx];
-    for (int idx = tid; idx < m.nseg; idx += BLOCK) seg_s[idx] = m.segs[idx];
-    for (int idx = tid; idx <= m.nslots; idx += BLOCK) slot_sph_s[idx] = m.slot_sph[idx];
-    for (int idx = tid; idx < S; idx += BLOCK) sph[idx] = m.sph[idx];
-    if (m.pad_lds)
-        for (int idx = tid; idx < 36 * S; idx += BLOCK) ((double*)(lds_raw + L.pad))[idx] = m.pad_pos[idx];
-    for (int idx = tid; idx < J; idx += BLOCK) {
-        hl_s[idx] = m.has_limits[idx];
-        jlim_s[2 * idx] = m.jmin[idx];
-        jlim_s[2 * idx + 1] = m.jmax[idx];
+    // the table image: every lane's loads go out together and land while the normals are
+    // drawn (or the trajectory is loaded); they are stored to LDS after that
+    double* zA = (double*)(lds_raw + L.nzA);
+    double* zB = (double*)(lds_raw + L.nzB);
+    const bool gen = a.fused_noise && !extra;
+    unsigned long long img[kCopyBatch];
+    const int nw = m.img_words;
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
+    if (gen) {
+        rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
+    } else {
+        const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
+        for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = prm[min(idx0 + tid + u * BLOCK, J * N - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (idx0 + tid + u * BLOCK < J * N) traj[idx0 + tid + u * BLOCK] = v[u];
+        }
     }
+    {
+        unsigned long long* dst = (unsigned long long*)(lds_raw + L.sph);
+#pragma unroll
+        for (int u = 0; u < kCopyBatch; ++u)
+            if (tid + u * BLOCK < nw) dst[tid + u * BLOCK] = img[u];
+        for (int w = tid + kCopyBatch * BLOCK; w < nw; w += BLOCK) dst[w] = m.img[w];
+    }
+    STAMP(6);
+    if (gen) rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
     if (tid == 0) flag = 0;
     __syncthreads();
     STAMP(1);
@@ -376,7 +369,7 @@ bool cost_supported(const DevModel& m)
 
 size_t rollout_lds_bytes(const DevModel& m, int pad_lds)
 {
-    return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, pad_lds).total;
+    return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, pad_lds).total;
 }
 
 size_t rollout_static_lds()
@@ -407,7 +400,7 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int blocks = a.num_noisy + (a.x_params ? 1 : 0);
     if (blocks <= 0) return;
-    const size_t lds = rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.pad_lds).total;
+    const size_t lds = rollout_lds_bytes(m, m.pad_lds);
     if (lds > 64 * 1024) {
         static size_t raised = 0;   // opt in to more than the default 64 KB once per size
         if (lds > raised) {

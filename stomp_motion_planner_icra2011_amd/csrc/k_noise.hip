@@ -1,5 +1,9 @@
 // k_noise.hip -- noise sampling, projection and control cost, fused per (rollout tile, joint).
 //
+// Generated rows are normally produced inside the rollout kernel (noise_device.h); this
+// kernel serves the reused rows (projection + control of re-based noise), the extra
+// noiseless rollout's control cost, and N > 128 where the fused phase does not apply.
+//
 //   eps = sigma_d * (0 + L z)          MultivariateGaussian::sample (multivariate_gaussian.h:88-94)
 //                                      via generateRollouts (policy_improvement.cpp:228-236)
 //   params = theta + eps               policy_improvement.cpp:234
@@ -13,54 +17,10 @@
 // z and eps sit in LDS as [k][RT] so one k costs RT/2 broadcast ds_read_b128.  Sums run
 // over k in ascending order, one rounding per operation (the oracle's contract); the
 // triangular product stops at k = i exactly like the oracle's loop.
-#include "kernels.h"
-#include "stomp_math.h"
+#include "noise_device.h"
 #include "stamps.h"
 
 namespace stomp {
-
-// acc[rr] += sum_{k < kend} AT[k][i] * v[k][rr], k ascending.  Unconditional clamped loads in
-// four 8-load batches that rotate roles without register copies, so three batches are in
-// flight while one is summed (a copy of the next batch into the current one would make
-// the compiler wait for the batch it has just issued).
-template <int RT>
-__device__ __forceinline__ void band_product(const double* __restrict__ AT, int N, int i, int kend,
-                                             const double* v, double* acc)
-{
-    // AT has kMatPadRows zero rows past N and v (LDS) kBandPad zero rows past N, so neither the
-    // loads nor the sums need clamping: terms past kend are exact no-ops (zeros of L^T above
-    // the diagonal or of the padding; the accumulator is never -0.0, see the caller)
-    constexpr int P = kBandBatch;
-    double A0[P], A1[P], A2[P], A3[P];
-    auto load = [&](double* buf, int k0) {
-#pragma unroll
-        for (int q = 0; q < P; ++q) buf[q] = AT[(size_t)(k0 + q) * N + i];
-    };
-    auto sum = [&](const double* buf, int k0) {
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const double* x = v + (k0 + q) * RT;
-#pragma unroll
-            for (int rr = 0; rr < RT; ++rr) acc[rr] += buf[q] * x[rr];
-        }
-    };
-    load(A0, 0);
-    load(A1, P);
-    load(A2, 2 * P);
-    for (int k0 = 0; k0 < kend; k0 += 4 * P) {
-        load(A3, k0 + 3 * P);
-        sum(A0, k0);
-        if (k0 + P >= kend) break;
-        load(A0, k0 + 4 * P);
-        sum(A1, k0 + P);
-        if (k0 + 2 * P >= kend) break;
-        load(A1, k0 + 5 * P);
-        sum(A2, k0 + 2 * P);
-        if (k0 + 3 * P >= kend) break;
-        load(A2, k0 + 6 * P);
-        sum(A3, k0 + 3 * P);
-    }
-}
 
 template <int BLOCK, int RT>
 __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
@@ -134,7 +94,7 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
         double acc[RT];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) acc[rr] = 0.0;
-        band_product<RT>(a.LT, N, i, wave_end, zs, acc);
+        band_product<RT>(a.LT, N, i, wave_end, zs, RT, acc);
         const double th = a.theta[(size_t)d * N + i];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
@@ -153,7 +113,7 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
         double acc[RT];
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) acc[rr] = 0.0;
-        band_product<RT>(a.MT, N, i, N, eps, acc);
+        band_product<RT>(a.MT, N, i, N, eps, RT, acc);
 #pragma unroll
         for (int rr = 0; rr < RT; ++rr) {
             const int r = r0 + rr;
@@ -170,26 +130,8 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     __syncthreads();
 
     for (int ii = tid; ii < Nall; ii += BLOCK) {
-        // the 7-tap window of every rollout first (all LDS reads in flight), then the sums over
-        // the taps inside [0, Nall) in ascending order
 #pragma unroll
-        for (int rr = 0; rr < RT; ++rr) {
-            double xw[7];
-#pragma unroll
-            for (int q = 0; q < 7; ++q) xw[q] = xs[rr * Nall + min(max(ii - 3 + q, 0), Nall - 1)];
-            double call = 0.0;
-#pragma unroll
-            for (int rule = 0; rule < 3; ++rule) {
-                const double wr = a.wr[rule];
-                if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
-                double s = 0.0;
-#pragma unroll
-                for (int q = 0; q < 7; ++q)
-                    if (ii - 3 + q >= 0 && ii - 3 + q < Nall) s += a.dcoef[rule][q] * xw[q];
-                call += wr * (s * s);
-            }
-            cs[rr * Nall + ii] = call;
-        }
+        for (int rr = 0; rr < RT; ++rr) cs[rr * Nall + ii] = control_term(a, xs + rr * Nall, Nall, ii);
     }
     __syncthreads();
     STAMP(4);
@@ -199,15 +141,7 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
         for (int rr = 0; rr < RT; ++rr) {
             const int r = r0 + rr;
             if (r >= a.K_loc) continue;
-            const double* c = cs + rr * Nall;
-            double o = c[i + 6];
-            if (N == 1) {
-                for (int q = 0; q < 6; ++q) { o += c[q]; o += c[Nall - 1 - q]; }
-            } else if (i == 0) {
-                for (int q = 0; q < 6; ++q) o += c[q];
-            } else if (i == N - 1) {
-                for (int q = 0; q < 6; ++q) o += c[Nall - 1 - q];
-            }
+            const double o = control_cost(cs + rr * Nall, N, Nall, i);
             a.control[((size_t)r * J + d) * N + i] = o;
         }
     }

@@ -279,9 +279,13 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
         for (int q = 0; q < B; ++q) buf[q] = MT[(size_t)min(k0 + q, N - 1) * N + i];
     };
     auto sum = [&](const double* buf, int k0) {
+        double x[B];   // the batch's LDS reads all issued before the first product
+#pragma unroll
+        for (int q = 0; q < B; ++q) x[q] = us[min(k0 + q, N - 1)];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < B; ++q)
-            if (k0 + q < N) s += buf[q] * us[k0 + q];
+            if (k0 + q < N) s += buf[q] * x[q];
     };
     load(A0, 0);
     load(A1, B);

@@ -23,9 +23,10 @@ constexpr int kRunMaxLarge = 8;   // spheres per FK op when N > 128
 constexpr int kSaves = 2;         // saved branch-point FK frames (LDS, one column per waypoint)
 constexpr int kSumBlock = 64;     // canonical blocked summation over rollouts
 constexpr int kBandBatch = 8;     // rows per load batch of the noise band products
-constexpr int kMatPadRows = 7 * kBandBatch;   // zero rows past N in LT / MT (ring look-ahead)
+constexpr int kMatPadRows = 12 * kBandBatch;  // zero rows past N in LT / MT (chunk + ring look-ahead)
 constexpr int kVelTap0 = 2;       // non-zero taps of the velocity rule DIFF_RULES[0]
 constexpr int kVelTap1 = 5;       // (stomp_utils.h:54), checked in stomp_engine_create
+constexpr int kNoiseJT = 8;       // joints per tile of the rollout kernel's noise phase (2 x 4 per lane)
 
 inline int run_max(int N) { return N <= 128 ? kRunMaxSmall : kRunMaxLarge; }
 
@@ -59,6 +60,8 @@ struct DevModel {
     int J, N, Nall, S, nops, nseg, nslots, sph_chunk;   // sph_chunk: most spheres on one segment
     int nsaves;                 // saved branch-point frames the FK program uses (0..kSaves, LDS)
     int pad_lds;                // padding-row positions staged in LDS (1) or read from HBM (0)
+    const unsigned long long* img;   // the rollout kernel's LDS table image (RolloutLds from .sph on)
+    int img_words;              // 8-byte words of it copied to LDS (up to .pad, or .total with pad_lds)
     const DevSegment* segs;
     const DevSphere* sph;
     const FkOp* ops;
@@ -72,11 +75,47 @@ struct DevModel {
     double vel_coef[7];         // invTime * DIFF_RULES[0][k]
     double w_obs, w_con, w_tq;
     int pad_collision;
-    const int* has_limits;      // [J]
-    const double* jmin;         // [J]
-    const double* jmax;         // [J]
     const double* QT;           // [J][N][N]
 };
+
+// LDS carve-up of the rollout kernel (bytes).  traj stays resident; the per-slot FK buffers
+// follow it and the noise phase's two buffers alias them (they are dead before the first
+// frame is published).  From .sph on the layout is a byte image that the engine assembles
+// once in HBM (DevModel::img, padding positions last) and each workgroup copies in one pass.
+struct RolloutLds {
+    size_t traj, fb, sv, av, nzl, nzA, nzB, sph, seg, ops, slot, hl, jlim, pad, total;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline int noise_jp(int J) { return (J + kNoiseJT - 1) / kNoiseJT * kNoiseJT; }
+
+__host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_slot, int nsaves, int nseg, int nops,
+                                                  int nslots, int pad_lds)
+{
+    RolloutLds l;
+    l.traj = 0;
+    l.fb = l.traj + (size_t)J * N * sizeof(double);
+    l.sv = l.fb + (size_t)12 * N * sizeof(double);
+    l.av = l.sv + (size_t)nsaves * 12 * N * sizeof(double);
+    l.nzl = l.av + (size_t)max_slot * N * sizeof(double);
+    // noise phase: A = z then x (padded), B = eps then the control-cost terms
+    const size_t nzw = (size_t)(N + kBandBatch) * noise_jp(J) > (size_t)J * (N + 12)
+                           ? (size_t)(N + kBandBatch) * noise_jp(J) : (size_t)J * (N + 12);
+    l.nzA = l.fb;
+    l.nzB = l.nzA + nzw * sizeof(double);
+    size_t end = l.nzl + (size_t)max_slot * N * sizeof(unsigned short);
+    if (l.nzB + nzw * sizeof(double) > end) end = l.nzB + nzw * sizeof(double);
+    l.sph = align16(end);
+    l.seg = align16(l.sph + (size_t)S * sizeof(DevSphere));
+    l.ops = align16(l.seg + (size_t)nseg * sizeof(DevSegment));
+    l.slot = align16(l.ops + (size_t)nops * sizeof(FkOp));
+    l.hl = align16(l.slot + (size_t)(nslots + 1) * sizeof(int));
+    l.jlim = align16(l.hl + (size_t)J * sizeof(int));
+    l.pad = align16(l.jlim + (size_t)2 * J * sizeof(double));
+    l.total = l.pad + (pad_lds ? (size_t)36 * S * sizeof(double) : 0);
+    return l;
+}
 
 struct Sigma {
     double v[kMaxJoints];
@@ -103,6 +142,8 @@ struct NoiseArgs {
 // Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
 // x_params) evaluates the noiseless rollout of theta (pipelined from the previous iteration).
 struct CostArgs {
+    int fused_noise;            // blocks < num_noisy first generate their row (NoiseArgs nz):
+    NoiseArgs nz;               // normals, L z, params, M eps, control costs (k_noise's work)
     const double* params;
     long long stride;
     int num_noisy;

@@ -1,0 +1,267 @@
+// noise_device.h -- the noise band products and the rollout kernel's fused noise phase.
+//
+//   eps = sigma_d * (0 + L z)          MultivariateGaussian::sample (multivariate_gaussian.h:88-94)
+//                                      via generateRollouts (policy_improvement.cpp:228-236)
+//   params = theta + eps               policy_improvement.cpp:234
+//   nproj = M eps                      computeProjectedNoise (policy_improvement.cpp:473-482)
+//   control = sum_i w_i (D_i x)^2      computeControlCosts (covariant_trajectory_policy.cpp:228-255),
+//                                      x = padded (params + nproj), 7-tap stencils instead of dense D_i
+//
+// Sums run over k in ascending order with one rounding per operation (the oracle's
+// contract); the triangular product adds only exact zeros past k = i.
+#pragma once
+
+#include "kernels.h"
+#include "stamps.h"
+#include "stomp_math.h"
+
+namespace stomp {
+
+// acc[rr] += sum_{k < kend} AT[k][i] * v[k * vstride + rr], k ascending.  Unconditional loads
+// in four 8-load batches that rotate roles without register copies, so three batches are in
+// flight while one is summed (a copy of the next batch into the current one would make the
+// compiler wait for the batch it has just issued).  AT has kMatPadRows zero rows past N and v
+// kBandBatch zero rows past N, so neither the loads nor the sums need clamping: terms past
+// kend are exact no-ops (zeros of L^T above the diagonal or of the padding; the accumulator
+// starts at +0.0 and is never -0.0, so adding +-0.0 leaves it unchanged).
+template <int RT>
+__device__ __forceinline__ void band_product(const double* __restrict__ AT, int N, int i, int kend,
+                                             const double* v, int vstride, double* acc)
+{
+    constexpr int P = kBandBatch;
+    double A0[P], A1[P], A2[P], A3[P];
+    auto load = [&](double* buf, int k0) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) buf[q] = AT[(size_t)(k0 + q) * N + i];
+    };
+    auto sum = [&](const double* buf, int k0) {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const double* x = v + (k0 + q) * vstride;
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr) acc[rr] += buf[q] * x[rr];
+        }
+    };
+    load(A0, 0);
+    load(A1, P);
+    load(A2, 2 * P);
+    for (int k0 = 0; k0 < kend; k0 += 4 * P) {
+        load(A3, k0 + 3 * P);
+        sum(A0, k0);
+        if (k0 + P >= kend) break;
+        load(A0, k0 + 4 * P);
+        sum(A1, k0 + P);
+        if (k0 + 2 * P >= kend) break;
+        load(A1, k0 + 5 * P);
+        sum(A2, k0 + 2 * P);
+        if (k0 + 3 * P >= kend) break;
+        load(A2, k0 + 6 * P);
+        sum(A3, k0 + 3 * P);
+    }
+}
+
+// Register-blocked band product of the rollout kernel's noise phase: lane l of a wave owns
+// waypoints i_t = l + 64 t (t < TI) and RT joints d0 .. d0 + RT - 1:
+//   acc[t][rr] += sum_{k in [kbeg, kend)} AT[k][i_t] * v[k * vstride + rr]   (t >= T0), k ascending.
+// One broadcast LDS read of v[k] feeds TI * RT products and one AT row load TI * RT / TI, so
+// the VALU, not the LDS or the vector memory path, bounds it.  AT rows come through buffer
+// loads (scalar row offset, one VGPR column offset per t) in a rotating four-batch ring,
+// three batches ahead; whole batches only (no branch between a batch's load and its use,
+// which would let the compiler sink the load to the use): the batch past kend adds exact
+// zeros (AT zero rows past N, kMatPadRows >= 4 * 4 * kBandK; v zero rows up to N + kBandBatch).
+constexpr int kBandK = 4;   // rows per batch
+static_assert(kMatPadRows >= 4 * 4 * kBandK && kBandBatch >= kBandK, "band_tile padding");
+template <int TI, int T0, int RT>
+__device__ __forceinline__ void band_tile(const double* __restrict__ AT, int N, const int* col, int kbeg, int kend,
+                                          const double* v, int vstride, double (*acc)[RT])
+{
+    constexpr int B = kBandK, NT = TI - T0;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)AT, 0, (int)((size_t)(N + kMatPadRows) * N * sizeof(double)), 0x00020000);
+    int ioff[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ioff[t] = col[T0 + t] * (int)sizeof(double);
+    double A0[B][NT], A1[B][NT], A2[B][NT], A3[B][NT];
+    auto load = [&](double (*buf)[NT], int k0) {
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                buf[q][t] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                           rsrc, ioff[t], (k0 + q) * N * (int)sizeof(double), 0));
+        __builtin_amdgcn_sched_barrier(0);   // keep the batch where it is issued
+    };
+    auto sum = [&](const double (*buf)[NT], int k0) {
+        double x[B][RT];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr) x[q][rr] = v[(k0 + q) * vstride + rr];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int rr = 0; rr < RT; ++rr) acc[T0 + t][rr] += buf[q][t] * x[q][rr];
+    };
+    const int nb = (kend - kbeg + B - 1) / B;
+    int k0 = kbeg, b = 0;
+    load(A0, k0);
+    load(A1, k0 + B);
+    load(A2, k0 + 2 * B);
+    for (; b + 4 <= nb; b += 4, k0 += 4 * B) {
+        load(A3, k0 + 3 * B); sum(A0, k0);
+        load(A0, k0 + 4 * B); sum(A1, k0 + B);
+        load(A1, k0 + 5 * B); sum(A2, k0 + 2 * B);
+        load(A2, k0 + 6 * B); sum(A3, k0 + 3 * B);
+    }
+    const int rem = nb - b;   // A0, A1, A2 hold the batches at k0, k0 + B, k0 + 2B
+    if (rem >= 1) sum(A0, k0);
+    if (rem >= 2) sum(A1, k0 + B);
+    if (rem >= 3) sum(A2, k0 + 2 * B);
+}
+
+// sum_rule wr * (D_rule x)^2 at padded index ii of one joint's padded trajectory x[0, Nall):
+// the 7-tap window first (all LDS reads in flight), then the sums over the taps inside
+// [0, Nall) in ascending order
+__device__ __forceinline__ double control_term(const NoiseArgs& a, const double* x, int Nall, int ii)
+{
+    double xw[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) xw[q] = x[min(max(ii - 3 + q, 0), Nall - 1)];
+    double call = 0.0;
+#pragma unroll
+    for (int rule = 0; rule < 3; ++rule) {
+        const double wr = a.wr[rule];
+        if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            if (ii - 3 + q >= 0 && ii - 3 + q < Nall) s += a.dcoef[rule][q] * xw[q];
+        call += wr * (s * s);
+    }
+    return call;
+}
+
+// control cost of free waypoint i from the padded per-index terms c[0, Nall): the first and
+// last free waypoints also collect the six padding terms on their side
+__device__ __forceinline__ double control_cost(const double* c, int N, int Nall, int i)
+{
+    double o = c[i + 6];
+    if (N == 1) {
+        for (int q = 0; q < 6; ++q) { o += c[q]; o += c[Nall - 1 - q]; }
+    } else if (i == 0) {
+        for (int q = 0; q < 6; ++q) o += c[q];
+    } else if (i == N - 1) {
+        for (int q = 0; q < 6; ++q) o += c[Nall - 1 - q];
+    }
+    return o;
+}
+
+// The whole generateRollouts + computeProjectedNoise + computeControlCosts work of local row
+// r, done by one BLOCK-wide workgroup before it executes the row, in two calls:
+// rollout_normals (z into zA) and rollout_project (writes the noise / params / control rows
+// to HBM and the parameters to traj[J][N] in LDS).  zA and zB are LDS buffers of
+// max((N + kBandBatch) * JP, J * Nall) doubles; JP = J rounded up to kNoiseJT.  N <= 128
+// (BLOCK = 256: four waves of 32 waypoints; the engine runs the fused phase only then).
+template <int BLOCK>
+__device__ __forceinline__ void rollout_normals(const NoiseArgs& a, int r, double* zA, double* zB, int tid)
+{
+    const int J = a.J, N = a.N, JP = noise_jp(J);
+    const int NB = N + kBandBatch;
+    const int g = a.first_global + r;
+    double* zs = zA;    // [NB][JP] standard normals
+    double* eps = zB;   // [NB][JP] noise (padding zeroed here)
+    for (int idx = tid; idx < NB * JP; idx += BLOCK) {
+        const int k = idx / JP, d = idx - k * JP;
+        if (k >= N || d >= J) { zs[idx] = 0.0; eps[idx] = 0.0; }
+    }
+    {
+        const int P = (N + 1) / 2;
+        for (int idx = tid; idx < J * P; idx += BLOCK) {
+            const int d = idx / P, p = idx - d * P;
+            double z0, z1;
+            normal_pair(a.seed, a.iteration, d, g, p, &z0, &z1);
+            zs[(2 * p) * JP + d] = z0;
+            if (2 * p + 1 < N) zs[(2 * p + 1) * JP + d] = z1;
+        }
+    }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
+                                                int tid)
+{
+    constexpr int RT = 4;   // joints per lane
+    const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J);
+    const size_t row = (size_t)r * J * N;
+    const double* zs = zA;
+    double* eps = zB;
+    __syncthreads();   // the normals are complete
+    STAMP(7);
+
+    // Lane l of wave w owns waypoint i = 32 w + (l & 31) and joints h * 4 .. h * 4 + 3 of each
+    // 8-joint tile (h = l >> 5): a matrix row's element is loaded once per workgroup, not once
+    // per joint tile, which is what bounds this phase (L2 -> CU bandwidth), and each load
+    // feeds four products.
+    const int wv = tid >> 6, lane = tid & 63;
+    const int i = 32 * wv + (lane & 31), h = lane >> 5;
+    int col[1] = {min(i, N - 1)};
+    const int ntile = JP / kNoiseJT;
+    // L is lower triangular: the wave's waypoints need rows k < 32 w + 32 only
+    const int lz_end = min(N, 32 * wv + 32);
+    for (int tl = 0; tl < ntile; ++tl) {
+        const int d0 = tl * kNoiseJT + h * RT;
+        double acc[1][RT];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) acc[0][rr] = 0.0;
+        band_tile<1, 0, RT>(a.LT, N, col, 0, lz_end, zs + d0, JP, acc);
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            const int d = d0 + rr;
+            if (d >= J || i >= N) continue;
+            const double e = a.sigma.v[d] * (0.0 + acc[0][rr]);
+            const double p = a.theta[(size_t)d * N + i] + e;
+            a.noise[row + (size_t)d * N + i] = e;
+            a.params[row + (size_t)d * N + i] = p;
+            traj[d * N + i] = p;
+            eps[i * JP + d] = e;
+        }
+    }
+    __syncthreads();
+
+    STAMP(8);
+    double* xs = zA;   // z is dead
+    for (int tl = 0; tl < ntile; ++tl) {
+        const int d0 = tl * kNoiseJT + h * RT;
+        double acc[1][RT];
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) acc[0][rr] = 0.0;
+        band_tile<1, 0, RT>(a.MT, N, col, 0, N, eps + d0, JP, acc);
+#pragma unroll
+        for (int rr = 0; rr < RT; ++rr) {
+            const int d = d0 + rr;
+            if (d >= J || i >= N) continue;
+            xs[d * Nall + i + 6] = traj[d * N + i] + acc[0][rr];
+        }
+    }
+    for (int idx = tid; idx < J * 12; idx += BLOCK) {
+        const int d = idx / 12, k = idx - d * 12;
+        xs[d * Nall + (k < 6 ? k : N + k)] = k < 6 ? a.start[d] : a.goal[d];
+    }
+    __syncthreads();
+
+    STAMP(9);
+    double* cs = zB;   // eps is dead
+    for (int idx = tid; idx < J * Nall; idx += BLOCK) {
+        const int d = idx / Nall, ii = idx - d * Nall;
+        cs[idx] = control_term(a, xs + d * Nall, Nall, ii);
+    }
+    __syncthreads();
+    for (int idx = tid; idx < J * N; idx += BLOCK) {
+        const int d = idx / N, t = idx - d * N;
+        a.control[row + idx] = control_cost(cs + d * Nall, N, Nall, t);
+    }
+}
+
+}  // namespace stomp

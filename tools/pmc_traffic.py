@@ -5,7 +5,7 @@ summary bench.py reports as roofline.traffic.
 Counters (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are KiB per
 dispatch from the L2's memory-side request counters (Infinity-Cache hits included);
 on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled.  The
-rollout-cost stage is two kernels (k_fk + k_pairs); its traffic is their sum.
+rollout-cost stage is the fused k_rollout kernel (one launch per iteration).
 
 Usage: python tools/pmc_traffic.py <pmc dir> <out.json>
 """
@@ -43,13 +43,13 @@ def main():
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             e["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0), 4)
         kernels[k] = e
-    stage = [k for k in kernels if k.startswith("stomp::k_fk") or k.startswith("stomp::k_pairs")]
+    stage = [k for k in kernels if k.startswith("stomp::k_rollout")]
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE TCC_HIT_sum TCC_MISS_sum | SQ_* (separate passes), "
                   "bench.py --steps 40 --warmup 5 --no-timing; per-dispatch means",
         "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> B; Infinity-Cache hits are "
                       "counted (memory side of L2), so this is L2-miss traffic, an upper bound on HBM bytes",
-        "stage": "rollout_cost = k_fk + k_pairs",
+        "stage": "rollout_cost = k_rollout",
         "hbm_bytes_per_launch": sum(kernels[k].get("hbm_bytes", 0.0) for k in stage),
         "kernels": kernels,
     }

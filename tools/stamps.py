@@ -38,6 +38,7 @@ def show(name, block, labels):
     if not idx:
         print(name, "no stamps")
         return
+    idx = sorted(idx, key=lambda i: v[i])   # time order
     t0 = v[idx[0]]
     print(f"--- {name} block {block}: total {(v[idx[-1]] - t0)} cycles")
     prev = t0
@@ -50,12 +51,12 @@ def cost_label(i):
     if 10 <= i < 100:
         g, ph = (i - 10) // 4, (i - 10) % 4
         return f"slot {g}: " + ["FK + publish", "positions+gathers+pots", "velocity", "fold (lanes t<N)"][ph]
-    return {0: "start", 1: "tables loaded", 2: "joint limits", 3: "sincos", 4: "FK/pairs done",
-            5: "end"}.get(i, str(i))
+    return {0: "start", 6: "normals / traj + tables", 7: "normals barrier", 8: "L z", 9: "M eps", 1: "control", 2: "joint limits", 3: "traj out",
+            4: "FK/pairs done", 5: "end"}.get(i, str(i))
 
 
-show("cost", 0, cost_label)
-show("cost", K, cost_label)   # the pipelined noiseless rollout
+show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch
+show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
 show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
 show("weights", 0, lambda i: ["start", "load+minmax", "exp", "psum", "u partials", "end"][i])
 
