@@ -12,6 +12,7 @@
 // the K-sharded multi-GPU result bit-identical to one GPU: the W_MINMAX / W_PSUM / W_USUM
 // phases emit exactly the per-block partials the fused mode sums, and RCCL moves them.
 #include "kernels.h"
+#include "noise_device.h"
 #include "stomp_math.h"
 #include "stamps.h"
 
@@ -53,6 +54,16 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
     const int nel = K * TC;
     const int nb = (K + kSumBlock - 1) / kSumBlock;
     STAMP(0);
+    // the noise tile is only needed at the end; its loads go out first so they land while
+    // the costs are reduced and exponentiated (MINMAX / PSUM never read it)
+    double nz[EPT];
+    if (a.mode == W_FUSED || a.mode == W_USUM) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = min((tid + k * BLOCK) / TC, K - 1);
+            nz[k] = a.noise[(size_t)r * JN + colc];
+        }
+    }
 
     if (a.mode != W_USUM) {
         double lmn = __builtin_inf(), lmx = -__builtin_inf();
@@ -170,12 +181,6 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
     __syncthreads();
     STAMP(3);
     {
-        double nz[EPT];
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            const int r = min((tid + k * BLOCK) / TC, K - 1);
-            nz[k] = a.noise[(size_t)r * JN + colc];
-        }
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const int el = tid + k * BLOCK;
@@ -255,8 +260,9 @@ void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s)
 __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
                                                 int nb_total, double* theta)
 {
-    __shared__ double us[256];
+    __shared__ double us[256 + kBandBatch];
     const int d = blockIdx.x, i = threadIdx.x;
+    if (i < kBandBatch) us[N + i] = 0.0;
     const size_t JN = (size_t)J * N;
     if (i < N) {
         if (u_all) {
@@ -268,41 +274,13 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
         }
     }
     __syncthreads();
+    // k ascending, the noise phase's pinned buffer-load ring (M^T has kMatPadRows zero rows,
+    // us has kBandBatch zero rows past N); whole waves run it, lanes past N store nothing
+    int col[1] = {min(i, N - 1)};
+    double acc[1][1] = {{0.0}};
+    band_tile<1, 0, 1>(MT, N, col, 0, N, us, 1, acc);
+    const double s = acc[0][0];
     if (i >= N) return;
-    // k ascending; four 16-load batches rotate (no register copies), so three are in flight
-    // while one is summed
-    constexpr int B = 16;
-    double s = 0.0;
-    double A0[B], A1[B], A2[B], A3[B];
-    auto load = [&](double* buf, int k0) {
-#pragma unroll
-        for (int q = 0; q < B; ++q) buf[q] = MT[(size_t)min(k0 + q, N - 1) * N + i];
-    };
-    auto sum = [&](const double* buf, int k0) {
-        double x[B];   // the batch's LDS reads all issued before the first product
-#pragma unroll
-        for (int q = 0; q < B; ++q) x[q] = us[min(k0 + q, N - 1)];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < B; ++q)
-            if (k0 + q < N) s += buf[q] * x[q];
-    };
-    load(A0, 0);
-    load(A1, B);
-    load(A2, 2 * B);
-    for (int k0 = 0; k0 < N; k0 += 4 * B) {
-        load(A3, k0 + 3 * B);
-        sum(A0, k0);
-        if (k0 + B >= N) break;
-        load(A0, k0 + 4 * B);
-        sum(A1, k0 + B);
-        if (k0 + 2 * B >= N) break;
-        load(A1, k0 + 5 * B);
-        sum(A2, k0 + 2 * B);
-        if (k0 + 3 * B >= N) break;
-        load(A2, k0 + 6 * B);
-        sum(A3, k0 + 3 * B);
-    }
     theta[(size_t)d * N + i] += 1.0 * s;
 }
 

@@ -116,6 +116,16 @@ def test_cfg2_shape_one_iteration_bitwise():
     _compare_iteration(o, e, 2)
 
 
+@pytest.mark.parametrize("dof,waypoints,Kr", [(14, 100, 4), (7, 40, 0), (7, 65, 3), (7, 129, 0)])
+def test_fused_noise_shapes_bitwise(dof, waypoints, Kr):
+    # the rollout kernel's fused noise phase: two 8-joint tiles (14 DOF), one or two waypoint
+    # halves per wave (N = 39, 64, 128), reused rows priced by k_noise beside it
+    p = make(dof=dof, waypoints=waypoints, K=16, Kr=Kr)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+
+
 def test_waypoints_200_dual_arm_bitwise():
     p = make(dof=14, waypoints=200, K=64)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
