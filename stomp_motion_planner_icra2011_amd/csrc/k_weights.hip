@@ -210,6 +210,184 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
     STAMP(5);
 }
 
+// Row-coalesced variant: a workgroup owns TCW consecutive flat columns c = d * N + t of the
+// [K][J][N] rows, so every row of its tile is TCW * 8 contiguous bytes (a whole 128-B line at
+// TCW = 16) and a wave's load covers 64 / TCW rows of it; lane (rs, cc) holds rows
+// rs, rs + RS, ... of column cc in registers.  Same phases, modes and canonical sums as
+// k_weights.
+template <int TCW, int EPT>
+__global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
+{
+    constexpr int BLOCK = 256, RS = BLOCK / TCW;
+    extern __shared__ __attribute__((aligned(16))) double V[];   // [K_loc][TCW]
+    __shared__ double red0[BLOCK], red1[BLOCK];
+    __shared__ double part[BLOCK];
+    __shared__ double mn_s[TCW], den_s[TCW], ps_s[TCW];
+    const int N = a.N, J = a.J, K = a.K_loc;
+    const int JN = J * N;
+    const int tid = threadIdx.x, cc = tid % TCW, rs = tid / TCW;
+    // XCD-grouped tiles: workgroups are dealt round-robin over the 8 XCDs, so block b takes
+    // tile (b mod 8)-th group's (b / 8)-th tile and the tiles sharing a 128-B line of a row
+    // meet in one XCD's L2 instead of each fetching the line from memory
+    const int nt = gridDim.x, x = blockIdx.x & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int tile = x * q8 + min(x, r8) + (blockIdx.x >> 3);
+    const int c0 = tile * TCW, c = c0 + cc;
+    const bool colok = c < JN;
+    const int cl = min(c, JN - 1);
+    const int tcol = cl % N;
+    const int nb = (K + kSumBlock - 1) / kSumBlock;
+    STAMP(0);
+    double nz[EPT];
+    if (a.mode == W_FUSED || a.mode == W_USUM) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) nz[k] = a.noise[(size_t)min(rs + RS * k, K - 1) * JN + cl];
+    }
+    double v[EPT];
+    if (a.mode != W_USUM) {
+        double lmn = __builtin_inf(), lmx = -__builtin_inf();
+        if (a.cum) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) v[k] = a.cum[(size_t)min(rs + RS * k, K - 1) * JN + cl];
+        } else {
+            double w[EPT];
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                const int r = min(rs + RS * k, K - 1);
+                v[k] = a.state[(size_t)r * N + tcol];
+                w[k] = a.control[(size_t)r * JN + cl];
+            }
+            // every load of the tile in flight before the first add (left alone, the scheduler
+            // interleaves adds that wait on a few loads at a time: one memory latency each)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) v[k] += w[k];
+            STAMP(6);
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = rs + RS * k;
+            if (!colok) v[k] = 0.0;
+            if (r < K && colok) {
+                if (v[k] < lmn) lmn = v[k];
+                if (v[k] > lmx) lmx = v[k];
+            }
+        }
+        if (a.mode == W_PSUM) {
+            if (tid < TCW && colok) {
+                red0[tid] = -a.mm[JN + c];
+                red1[tid] = a.mm[c];
+            }
+        } else {
+            red0[tid] = lmn;
+            red1[tid] = lmx;
+            __syncthreads();
+            if (tid < TCW) {
+                double mn = red0[tid], mx = red1[tid];
+                for (int j0 = tid + TCW; j0 < BLOCK; j0 += 16 * TCW) {
+                    double x0[16], x1[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int j = min(j0 + q * TCW, BLOCK - TCW + tid);   // stays in this column
+                        x0[q] = red0[j];
+                        x1[q] = red1[j];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {   // order-free; the clamped repeats are harmless
+                        if (x0[q] < mn) mn = x0[q];
+                        if (x1[q] > mx) mx = x1[q];
+                    }
+                }
+                red0[tid] = mn;
+                red1[tid] = mx;
+                if (a.mode == W_MINMAX && colok) {
+                    a.mm[c] = mx;
+                    a.mm[JN + c] = -mn;
+                }
+            }
+            if (a.mode == W_MINMAX) return;
+        }
+        __syncthreads();
+        if (tid < TCW) {
+            double den = red1[tid] - red0[tid];
+            if (den < 1e-8) den = 1e-8;
+            den_s[tid] = den;
+            mn_s[tid] = red0[tid];
+        }
+        __syncthreads();
+        STAMP(1);
+        const double mn = mn_s[cc], den = den_s[cc];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = rs + RS * k;
+            v[k] = det_exp(-10.0 * (v[k] - mn) / den);
+            if (r < K) V[r * TCW + cc] = v[k];
+        }
+        __syncthreads();
+        STAMP(2);
+        if (tid < nb * TCW) {
+            const int b = tid / TCW, c2 = tid % TCW;
+            const int r1 = min(K, (b + 1) * kSumBlock);
+            const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TCW + c2, TCW, r1 - b * kSumBlock);
+            part[tid] = s;
+            if (a.mode == W_PSUM && c0 + c2 < JN) a.psum_part[(size_t)b * JN + c0 + c2] = s;
+        }
+        if (a.mode == W_PSUM) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                const int r = rs + RS * k;
+                if (r < K && colok) a.prob[(size_t)r * JN + c] = v[k];
+            }
+            return;
+        }
+        __syncthreads();
+        if (tid < TCW) {
+            double ps = 0.0;
+            for (int b = 0; b < nb; ++b) ps += part[b * TCW + tid];
+            ps_s[tid] = ps;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) v[k] = colok ? a.prob[(size_t)min(rs + RS * k, K - 1) * JN + cl] : 0.0;
+        if (tid < TCW) {
+            double ps = 0.0;
+            if (colok)
+                for (int b = 0; b < a.nb_total; ++b) ps += a.psum_all[(size_t)b * JN + c];
+            ps_s[tid] = ps;
+        }
+    }
+    __syncthreads();
+    STAMP(3);
+    {
+        const double ps = ps_s[cc];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = rs + RS * k;
+            if (r >= K) continue;
+            if (!colok) { V[r * TCW + cc] = 0.0; continue; }
+            const double pn = v[k] / ps;
+            a.prob[(size_t)r * JN + c] = pn;
+            V[r * TCW + cc] = nz[k] * pn;
+        }
+    }
+    __syncthreads();
+    if (tid < nb * TCW) {
+        const int b = tid / TCW, c2 = tid % TCW;
+        const int r1 = min(K, (b + 1) * kSumBlock);
+        const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TCW + c2, TCW, r1 - b * kSumBlock);
+        part[tid] = s;
+        if (a.mode == W_USUM && c0 + c2 < JN) a.u_part[(size_t)b * JN + c0 + c2] = s;
+    }
+    if (a.mode == W_USUM) return;
+    __syncthreads();
+    STAMP(4);
+    if (tid < TCW && colok) {
+        double u = 0.0;
+        for (int b = 0; b < nb; ++b) u += part[b * TCW + tid];
+        a.u[c] = u;
+    }
+    STAMP(5);
+}
+
 STOMP_STAMP_ACCESSORS(weights)
 
 // columns per workgroup: as many as keep K_loc * TC <= 2048 (more workgroups, shorter
@@ -224,8 +402,37 @@ int weights_tile(int K_loc)
     return tc;
 }
 
+#ifndef WEIGHTS_ROWS_TCW
+#define WEIGHTS_ROWS_TCW 4
+#endif
+template <int EPT>
+static void launch_rows(const WeightArgs& a, hipStream_t s)
+{
+    constexpr int TCW = WEIGHTS_ROWS_TCW;
+    const int JN = a.J * a.N;
+    const size_t lds = (size_t)a.K_loc * TCW * sizeof(double);
+    static size_t raised = 0;   // opt in to more than the default 64 KB once per size
+    if (lds > 48 * 1024 && lds > raised) {
+        (void)hipFuncSetAttribute((const void*)k_weights_rows<TCW, EPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        raised = lds;
+    }
+    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3((JN + TCW - 1) / TCW), dim3(256), lds, s, a);
+}
+
 void launch_weights(const WeightArgs& a, hipStream_t s)
 {
+#ifndef WEIGHTS_COLUMN_TILES
+    // row-coalesced flat-column tiles while a lane's rows fit its registers
+    constexpr int RS = 256 / WEIGHTS_ROWS_TCW;
+    const int nb = (a.K_loc + kSumBlock - 1) / kSumBlock;
+    if (nb * WEIGHTS_ROWS_TCW <= 256) {
+        if (a.K_loc <= 4 * RS) return launch_rows<4>(a, s);
+        if (a.K_loc <= 8 * RS) return launch_rows<8>(a, s);
+        if (a.K_loc <= 16 * RS) return launch_rows<16>(a, s);
+        if (a.K_loc <= 32 * RS) return launch_rows<32>(a, s);
+    }
+#endif
     dim3 grid((a.N + a.tc - 1) / a.tc, a.J);
     const size_t lds = (size_t)a.K_loc * a.tc * sizeof(double);
     if ((size_t)a.K_loc * a.tc <= 2048 && WEIGHTS_TILE_ELEMS <= 2048)

@@ -58,7 +58,7 @@ def cost_label(i):
 show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch
 show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
 show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
-show("weights", 0, lambda i: ["start", "load+minmax", "exp", "psum", "u partials", "end"][i])
+show("weights", 0, lambda i: ["start", "min/max", "exp", "psum", "u partials", "end", "tile loaded"][i])
 
 
 def residency():
