@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -42,6 +43,7 @@ struct stomp_engine {
     bool own_stream = false;
     int J = 0, N = 0, Nall = 0, K = 0, Kr = 0, K_loc = 0, first = 0, S = 0, nseg = 0;
     int world = 1, rank = 0;
+    bool split_modes = false;   // weights in the MINMAX / PSUM / USUM phases (world > 1, or the debug hook)
     uint64_t seed = 0;
     double disc = 0.05, w_smooth = 0, w_obs = 0, w_con = 0, w_tq = 0;
     double smooth[3] = {0, 0, 0};
@@ -358,28 +360,43 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     {
         Timed tm(e, T_WEIGHTS);
         if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
-        if (e->world == 1) {
+        if (!e->split_modes) {
             wa.mode = W_FUSED;
             launch_weights(wa, e->stream);
         } else {
-#ifdef STOMP_WITH_RCCL
+            // the sharded decomposition; with one rank (debug hook) the all-reduce is the
+            // identity and the all-gathers are device copies
             const size_t JN = (size_t)e->J * e->N;
             const size_t nb_loc = (size_t)e->K_loc / kSumBlock;
             wa.mode = W_MINMAX;
             launch_weights(wa, e->stream);
-            NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
+#ifdef STOMP_WITH_RCCL
+            if (e->world > 1)
+                NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
+#endif
             wa.mode = W_PSUM;
             launch_weights(wa, e->stream);
-            NCCL_TRY(e, ncclAllGather(e->d_psum_part, e->d_psum_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
+#ifdef STOMP_WITH_RCCL
+            if (e->world > 1)
+                NCCL_TRY(e, ncclAllGather(e->d_psum_part, e->d_psum_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
+#endif
+            if (e->world == 1)
+                HIP_TRY(e, hipMemcpyAsync(e->d_psum_all, e->d_psum_part, sizeof(double) * nb_loc * JN,
+                                          hipMemcpyDeviceToDevice, e->stream));
             wa.mode = W_USUM;
             launch_weights(wa, e->stream);
-            NCCL_TRY(e, ncclAllGather(e->d_u_part, e->d_u_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
+#ifdef STOMP_WITH_RCCL
+            if (e->world > 1)
+                NCCL_TRY(e, ncclAllGather(e->d_u_part, e->d_u_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
 #endif
+            if (e->world == 1)
+                HIP_TRY(e, hipMemcpyAsync(e->d_u_all, e->d_u_part, sizeof(double) * nb_loc * JN,
+                                          hipMemcpyDeviceToDevice, e->stream));
         }
     }
     {
         Timed tm(e, T_UPDATE);
-        launch_update(e->J, e->N, e->d_MT, e->d_u, e->world > 1 ? e->d_u_all : nullptr, e->K / kSumBlock,
+        launch_update(e->J, e->N, e->d_MT, e->d_u, e->split_modes ? e->d_u_all : nullptr, e->K / kSumBlock,
                       e->d_theta, e->stream);
     }
     if (pipelined) {
@@ -465,6 +482,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     e->J = d->num_joints; e->N = d->num_time_steps; e->Nall = e->N + 2 * kPad;
     e->K = d->num_rollouts; e->Kr = d->num_reused_rollouts;
     e->world = world; e->rank = world > 1 ? d->rank : 0;
+    // STOMP_DEBUG_SHARDED_MODES=1: a one-device engine runs the multi-GPU weights phases
+    // (test hook for the MINMAX / PSUM / USUM kernels; needs whole 64-rollout blocks, no reuse)
+    {
+        const char* dbg = std::getenv("STOMP_DEBUG_SHARDED_MODES");
+        e->split_modes = world > 1 || (dbg && dbg[0] == '1' && d->num_rollouts % kSumBlock == 0 &&
+                                       d->num_reused_rollouts == 0);
+    }
     e->K_loc = e->K / world; e->first = e->rank * e->K_loc;
     if (e->K_loc > kSumBlock * 64) {
         rc = fail(e, STOMP_E_INVALID, "at most %d rollouts per device", kSumBlock * 64);
@@ -561,7 +585,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
     if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
-    if (world > 1) {
+    if (e->split_modes) {
         const size_t nb_loc = (size_t)e->K_loc / kSumBlock, nb_tot = (size_t)e->K / kSumBlock;
         CREATE_TRY(dev_alloc(e, &e->d_mm, 2 * (size_t)J * N));
         CREATE_TRY(dev_alloc(e, &e->d_psum_part, nb_loc * J * N));

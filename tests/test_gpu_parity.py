@@ -126,6 +126,17 @@ def test_fused_noise_shapes_bitwise(dof, waypoints, Kr):
         _compare_iteration(o, e, it)
 
 
+@pytest.mark.parametrize("K,cum", [(128, False), (192, True)])
+def test_sharded_weight_phases_bitwise(monkeypatch, K, cum):
+    # the multi-GPU weights decomposition (MINMAX -> all-reduce -> PSUM -> all-gather -> USUM ->
+    # all-gather -> update from block partials) on one device, collectives as identities/copies
+    monkeypatch.setenv("STOMP_DEBUG_SHARDED_MODES", "1")
+    p = make(K=K, Kr=0, use_cumulative_costs=cum)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+
+
 def test_waypoints_200_dual_arm_bitwise():
     p = make(dof=14, waypoints=200, K=64)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
