@@ -37,6 +37,10 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kPairUnroll = PAIR_UNROLL;   // (sphere, waypoint) pairs per lane in flight
 constexpr int kCopyBatch = 12;             // table-image words per lane per copy pass
+#ifndef SPHERE_UNROLL
+#define SPHERE_UNROLL 2
+#endif
+constexpr int kSphereUnroll = SPHERE_UNROLL;   // spheres per pair lane with gathers in flight
 }
 
 __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
@@ -199,6 +203,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     const int t_own = tid;                      // FK / fold lane: waypoint tid (tid < N)
     const int qb = tid / N, tb = tid - qb * N;  // first (sphere, waypoint) pair of this lane
     const int dq = BLOCK / N, dt = BLOCK - dq * N;
+    const int G = BLOCK / N, pg = tid / N, pt = tid - pg * N;   // pair lanes: (group, waypoint)
     // C: running frame in the registers of lanes t < N, reloaded from fb after each slot's
     // pairs so it is not live across them; branch-point frames saved in LDS (column t of sv)
     Frame C;
@@ -247,6 +252,52 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         // lane = consecutive (sphere, waypoint) pairs of the slot, kPairUnroll in flight
         // lane takes pairs (q, t) = (tid / N, tid % N) + k * BLOCK, stepped without dividing
         const int ns = se - sb;
+#ifndef PAIRS_STEPPED
+        // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
+        // flight) and serves spheres g, g + G, ... of the slot, kSphereUnroll gathers in flight
+        if (pg < G) {
+            double F[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
+            for (int q0 = pg; q0 < ns; q0 += G * kSphereUnroll) {
+                float dv[kSphereUnroll];
+#pragma unroll
+                for (int u = 0; u < kSphereUnroll; ++u) {
+                    const double* pos = sph[sb + min(q0 + u * G, ns - 1)].pos;
+                    double x[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+                        x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
+                    dv[u] = sdf_distance(m, x);
+                }
+                STAMP(40 + o.slot);
+#pragma unroll
+                for (int u = 0; u < kSphereUnroll; ++u) {
+                    const int q = q0 + u * G;
+                    const bool in = q < ns;
+                    double pot = 0.0;
+                    if (in) {
+                        const DevSphere& sp = sph[sb + q];
+                        const double dd = (double)dv[u];
+                        col |= dd <= sp.radius;
+                        pot = potential(sp, dd);
+                        av[q * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                    }
+                    // append (q, t) with pot != 0 to the slot's list: one LDS atomic per wave
+                    const bool nz = in && pot != 0.0;
+                    const unsigned long long mask = __ballot(nz);
+                    if (mask) {
+                        const int lane_id = tid & 63;
+                        const int leader = __ffsll((long long)mask) - 1;
+                        int base = 0;
+                        if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                        base = __shfl(base, leader, 64);
+                        if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
+                    }
+                }
+            }
+        }
+#else
         int q = qb, t = tb;
         while (q < ns) {
             int qq[kPairUnroll], tt[kPairUnroll];
@@ -265,6 +316,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                 apply_lds(fb, N, tt[u], sph[sb + min(qq[u], ns - 1)].pos, x);
                 dv[u] = sdf_distance(m, x);
             }
+            STAMP(40 + o.slot);
 #pragma unroll
             for (int u = 0; u < kPairUnroll; ++u) {
                 const bool in = qq[u] < ns;
@@ -293,6 +345,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 #endif
             }
         }
+#endif
         __syncthreads();   // pots and the non-zero list complete
         STAMP(11 + 4 * o.slot);
         // velocities only for the listed pairs, spread densely over the block

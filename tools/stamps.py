@@ -48,7 +48,9 @@ def show(name, block, labels):
 
 
 def cost_label(i):
-    if 10 <= i < 100:
+    if 40 <= i < 100:
+        return f"slot {i - 40}: gathers issued (last round)"
+    if 10 <= i < 40:
         g, ph = (i - 10) // 4, (i - 10) % 4
         return f"slot {g}: " + ["FK + publish", "positions+gathers+pots", "velocity", "fold (lanes t<N)"][ph]
     return {0: "start", 6: "normals / traj + tables", 7: "normals barrier", 8: "L z", 9: "M eps", 1: "control", 2: "joint limits", 3: "traj out",
