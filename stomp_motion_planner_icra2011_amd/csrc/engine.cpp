@@ -619,11 +619,16 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
                             m.sph_chunk, N));
         m.nsaves = 0;
         for (const FkOp& o : e->ops) m.nsaves = std::max(m.nsaves, o.save + 1);
-        // padding-row positions go to LDS only when that costs no workgroup per CU
+        // padding-row positions go to LDS unless that costs a workgroup per CU the launch
+        // would use: one rollout launch has K_loc + 1 workgroups over the device's CUs
         const size_t stat = rollout_static_lds();
         const size_t with_pad = rollout_lds_bytes(m, 1) + stat, without = rollout_lds_bytes(m, 0) + stat;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || cus <= 0)
+            cus = 256;
+        const int need = (e->K_loc + 1 + cus - 1) / cus;
         m.pad_lds = (with_pad <= kRolloutLdsMax &&
-                     rollout_blocks_per_cu(with_pad) >= rollout_blocks_per_cu(without)) ? 1 : 0;
+                     rollout_blocks_per_cu(with_pad) >= std::min(need, rollout_blocks_per_cu(without))) ? 1 : 0;
         const size_t lds = rollout_lds_bytes(m, m.pad_lds) + stat;
         if (lds > kRolloutLdsMax)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
