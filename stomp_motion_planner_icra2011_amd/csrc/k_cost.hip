@@ -83,6 +83,19 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
 }
 
+// max of x over the 64 lanes of the wave (every lane active): DPP within rows of 16, then
+// the four row results through scalar registers
+__device__ __forceinline__ unsigned wave_max_u32(unsigned x)
+{
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));    // quad_perm 1,0,3,2
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));    // quad_perm 2,3,0,1
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));   // row_half_mirror
+    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));   // row_mirror
+    const unsigned a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
+    const unsigned c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
+    return max(max(a, b), max(c, d));
+}
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
 {
@@ -167,8 +180,8 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
             const double* Q = m.QT + (size_t)j * N * N;
             double* tj = traj + j * N;
             for (int pass = 0; pass < 11; ++pass) {
-                double cand = -1.0;
-                int ci = 0x7fffffff;
+                double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
+                int ci = 0;
                 for (int t = lane; t < N; t += 64) {
                     const double v = tj[t];
                     double absamt = 0.0;
@@ -176,17 +189,30 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                     else if (v < jmin) absamt = fabs(jmin - v);
                     if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
                 }
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const double ov = __shfl_xor(cand, off, 64);
-                    const int oi = __shfl_xor(ci, off, 64);
-                    if (ov > cand || (ov == cand && oi < ci)) { cand = ov; ci = oi; }
+                // wave argmax, first index on ties: the bits of a non-negative double order like
+                // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
+                const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
+                const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
+                const unsigned mh = wave_max_u32(hi);
+                const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
+                if ((mh | ml) == 0u) break;   // no violation left (wave-uniform)
+                const bool match = hi == mh && lo == ml;
+                int cm = 0;
+                for (int blk = 0; blk * 64 < N; ++blk) {
+                    const unsigned long long b = __ballot(match && (ci >> 6) == blk);
+                    if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
                 }
-                if (cand < 0.0) break;   // wave-uniform
-                const double v = tj[ci];
+                const double* Qc = Q + (size_t)cm * N;
+                double qv[4];   // the column's loads go out with the diagonal's (N <= 256)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) qv[u] = Qc[min(lane + 64 * u, N - 1)];
+                const double qd = Qc[cm];
+                const double v = tj[cm];
                 const double amount = v > jmax ? jmax - v : jmin - v;
-                const double mult = amount / Q[(size_t)ci * N + ci];
-                for (int t = lane; t < N; t += 64) tj[t] += mult * Q[(size_t)ci * N + t];
+                const double mult = amount / qd;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (lane + 64 * u < N) tj[lane + 64 * u] += mult * qv[u];
                 __builtin_amdgcn_wave_barrier();
             }
         }
