@@ -71,6 +71,7 @@ __device__ __forceinline__ void band_product(const double* __restrict__ AT, int 
 // zeros (AT zero rows past N, kMatPadRows >= 4 * 4 * kBandK; v zero rows up to N + kBandBatch).
 constexpr int kBandK = 4;   // rows per batch
 static_assert(kMatPadRows >= 4 * 4 * kBandK && kBandBatch >= kBandK, "band_tile padding");
+constexpr int kCtlRun = 4;  // padded indices per lane in the rollout kernel's control stencils
 template <int TI, int T0, int RT>
 __device__ __forceinline__ void band_tile(const double* __restrict__ AT, int N, const int* col, int kbeg, int kend,
                                           const double* v, int vstride, double (*acc)[RT])
@@ -253,15 +254,49 @@ __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, doubl
 
     STAMP(9);
     double* cs = zB;   // eps is dead
-    for (int idx = tid; idx < J * Nall; idx += BLOCK) {
-        const int d = idx / Nall, ii = idx - d * Nall;
-        cs[idx] = control_term(a, xs + d * Nall, Nall, ii);
+    {
+        // lane = (joint, run of kCtlRun consecutive padded indices): one 7-tap window read
+        // serves the run; taps outside [0, Nall) are skipped as in control_term
+        constexpr int R = kCtlRun;
+        const int nrun = (Nall + R - 1) / R;
+        for (int item = tid; item < J * nrun; item += BLOCK) {
+            const int d = item / nrun, ii0 = (item - d * nrun) * R;
+            const double* x = xs + d * Nall;
+            double xw[R + 6];
+#pragma unroll
+            for (int q = 0; q < R + 6; ++q) xw[q] = x[min(max(ii0 - 3 + q, 0), Nall - 1)];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int ii = ii0 + u;
+                double call = 0.0;
+#pragma unroll
+                for (int rule = 0; rule < 3; ++rule) {
+                    const double wr = a.wr[rule];
+                    if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 7; ++q)
+                        if (ii - 3 + q >= 0 && ii - 3 + q < Nall) sacc += a.dcoef[rule][q] * xw[u + q];
+                    call += wr * (sacc * sacc);
+                }
+                if (ii < Nall) cs[d * Nall + ii] = call;
+            }
+        }
     }
+    STAMP(61);
     __syncthreads();
-    for (int idx = tid; idx < J * N; idx += BLOCK) {
-        const int d = idx / N, t = idx - d * N;
-        a.control[row + idx] = control_cost(cs + d * Nall, N, Nall, t);
+    STAMP(62);
+    {
+        constexpr int R = kCtlRun;
+        const int nrun = (N + R - 1) / R;
+        for (int item = tid; item < J * nrun; item += BLOCK) {
+            const int d = item / nrun, t0 = (item - d * nrun) * R;
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (t0 + u < N) a.control[row + (size_t)d * N + t0 + u] = control_cost(cs + d * Nall, N, Nall, t0 + u);
+        }
     }
+    STAMP(63);
 }
 
 }  // namespace stomp
