@@ -32,10 +32,6 @@ constexpr int kBlock = 256;
 #ifndef ROLLOUT_MIN_WAVES
 #define ROLLOUT_MIN_WAVES 3
 #endif
-#ifndef PAIR_UNROLL
-#define PAIR_UNROLL 4
-#endif
-constexpr int kPairUnroll = PAIR_UNROLL;   // (sphere, waypoint) pairs per lane in flight
 constexpr int kCopyBatch = 12;             // table-image words per lane per copy pass
 #ifndef SPHERE_UNROLL
 #define SPHERE_UNROLL 2
@@ -227,44 +223,54 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 
     // ---- FK program, slot by slot, with the slot's pairs in between
     const int t_own = tid;                      // FK / fold lane: waypoint tid (tid < N)
-    const int qb = tid / N, tb = tid - qb * N;  // first (sphere, waypoint) pair of this lane
-    const int dq = BLOCK / N, dt = BLOCK - dq * N;
     const int G = BLOCK / N, pg = tid / N, pt = tid - pg * N;   // pair lanes: (group, waypoint)
-    // C: running frame in the registers of lanes t < N, reloaded from fb after each slot's
-    // pairs so it is not live across them; branch-point frames saved in LDS (column t of sv)
+    // C: running frame in the registers of lanes t < N; branch-point frames saved in LDS
+    // (column t of sv).  Lanes t < N are also pair lanes (0, t).
     Frame C;
     double cum = 0.0, state = 0.0;
     bool col = false;
-    for (int op = 0; op < m.nops; ++op) {
-        const FkOp o = ops_s[op];
-        if (o.seg >= 0 && t_own < N) {
-            const DevSegment& sg = seg_s[o.seg];
-            double st = 0.0, ct = 1.0;
-            if (sg.q_index >= 0) det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
-            Frame nf;
-            if (o.base == kBaseChain) {
-                compose(sg, &C, st, ct, nf);
-            } else if (o.base == kBaseRoot) {
-                compose(sg, nullptr, st, ct, nf);
-            } else {
-                Frame pf;
-                const double* src = sv + (size_t)o.base * 12 * N + t_own;
+    // one FK program step (stomp_optimizer.cpp via treefksolverjointposaxis_partial.cpp:108-140)
+    auto fk_op = [&](const FkOp& o) {
+        if (o.seg < 0 || t_own >= N) return;
+        const DevSegment& sg = seg_s[o.seg];
+        double st = 0.0, ct = 1.0;
+        if (sg.q_index >= 0) det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
+        Frame nf;
+        if (o.base == kBaseChain) {
+            compose(sg, &C, st, ct, nf);
+        } else if (o.base == kBaseRoot) {
+            compose(sg, nullptr, st, ct, nf);
+        } else {
+            Frame pf;
+            const double* src = sv + (size_t)o.base * 12 * N + t_own;
 #pragma unroll
-                for (int k = 0; k < 9; ++k) pf.R[k] = src[k * N];
+            for (int k = 0; k < 9; ++k) pf.R[k] = src[k * N];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) pf.p[k] = src[(9 + k) * N];
-                compose(sg, &pf, st, ct, nf);
-            }
-            C = nf;
-            if (o.save >= 0) {
-                double* dst = sv + (size_t)o.save * 12 * N + t_own;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) dst[k * N] = C.R[k];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
-            }
+            for (int k = 0; k < 3; ++k) pf.p[k] = src[(9 + k) * N];
+            compose(sg, &pf, st, ct, nf);
         }
-        if (o.slot < 0) continue;   // uniform: not a sphere-carrying segment
+        C = nf;
+        if (o.save >= 0) {
+            double* dst = sv + (size_t)o.save * 12 * N + t_own;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) dst[k * N] = C.R[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
+        }
+    };
+    // run the program from op up to and including the next sphere-carrying segment; its
+    // index (or nops) is uniform
+    auto fk_advance = [&](int op) -> int {
+        for (; op < m.nops; ++op) {
+            const FkOp o = ops_s[op];
+            fk_op(o);
+            if (o.slot >= 0) return op;
+        }
+        return m.nops;
+    };
+    int op = fk_advance(0);
+    while (op < m.nops) {
+        const FkOp o = ops_s[op];
         if (t_own < N) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) fb[k * N + t_own] = C.R[k];
@@ -275,10 +281,8 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         __syncthreads();   // frame published; every lane's previous fold is done
         STAMP(10 + 4 * o.slot);
         const int sb = slot_sph_s[o.slot], se = slot_sph_s[o.slot + 1];
-        // lane = consecutive (sphere, waypoint) pairs of the slot, kPairUnroll in flight
-        // lane takes pairs (q, t) = (tid / N, tid % N) + k * BLOCK, stepped without dividing
         const int ns = se - sb;
-#ifndef PAIRS_STEPPED
+        int next = -1;
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
         // flight) and serves spheres g, g + G, ... of the slot, kSphereUnroll gathers in flight
         if (pg < G) {
@@ -297,6 +301,13 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                     dv[u] = sdf_distance(m, x);
                 }
                 STAMP(40 + o.slot);
+#ifdef FK_PIPELINE
+                // while the first gathers are in flight, lanes t < N run the FK program on to
+                // the next slot's frame (C; the published frame stays in fb for this slot).
+                // Off by default: at the 168-VGPR cap the frame spills, and the spill reloads
+                // wait on the gathers (one vmcnt counter)
+                if (next < 0) next = fk_advance(op + 1);
+#endif
 #pragma unroll
                 for (int u = 0; u < kSphereUnroll; ++u) {
                     const int q = q0 + u * G;
@@ -323,63 +334,21 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                 }
             }
         }
-#else
-        int q = qb, t = tb;
-        while (q < ns) {
-            int qq[kPairUnroll], tt[kPairUnroll];
-            float dv[kPairUnroll];
-#pragma unroll
-            for (int u = 0; u < kPairUnroll; ++u) {
-                qq[u] = q;
-                tt[u] = t;
-                q += dq;
-                t += dt;
-                if (t >= N) { t -= N; ++q; }
-            }
-#pragma unroll
-            for (int u = 0; u < kPairUnroll; ++u) {
-                double x[3];
-                apply_lds(fb, N, tt[u], sph[sb + min(qq[u], ns - 1)].pos, x);
-                dv[u] = sdf_distance(m, x);
-            }
-            STAMP(40 + o.slot);
-#pragma unroll
-            for (int u = 0; u < kPairUnroll; ++u) {
-                const bool in = qq[u] < ns;
-                double pot = 0.0;
-                if (in) {
-                    const DevSphere& sp = sph[sb + qq[u]];
-                    const double dd = (double)dv[u];
-                    col |= dd <= sp.radius;
-                    pot = potential(sp, dd);
-                    av[qq[u] * N + tt[u]] = pot;   // a = pot * |v| is +0 exactly when pot == +0
-                }
-#ifndef NO_COMPACT
-                // append (q, t) with pot != 0 to the slot's list: one LDS atomic per wave
-                const bool nz = in && pot != 0.0;
-                const unsigned long long mask = __ballot(nz);
-                if (mask) {
-                    const int lane_id = tid & 63;
-                    const int leader = __ffsll((long long)mask) - 1;
-                    int base = 0;
-                    if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                    base = __shfl(base, leader, 64);
-                    if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(qq[u] * N + tt[u]);
-                }
-#else
-                if (in && pot != 0.0) av[qq[u] * N + tt[u]] = pot * sphere_speed(m, fb, pad, sph[sb + qq[u]], sb + qq[u], tt[u]);
-#endif
-            }
-        }
-#endif
         __syncthreads();   // pots and the non-zero list complete
         STAMP(11 + 4 * o.slot);
         // velocities only for the listed pairs, spread densely over the block
-#ifndef NO_COMPACT
         for (int i = tid; i < nz_count; i += BLOCK) {
             const int it = nzl[i];
             const int qi = it / N, ti = it - qi * N;
             av[it] *= sphere_speed(m, fb, pad, sph[sb + qi], sb + qi, ti);
+        }
+#ifndef FK_PIPELINE
+        // C is reloaded from fb (not kept live across the pairs)
+        if (t_own < N) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
         }
 #endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
@@ -398,11 +367,11 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                     state += cum;
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
         }
+        // lanes that ran no pair round (or the unpipelined build) advance here; the
+        // program's control flow is uniform, so every lane arrives at the same next op
+        if (next < 0) next = fk_advance(op + 1);
+        op = next;
         STAMP(13 + 4 * o.slot);
     }
     STAMP(4);
