@@ -23,7 +23,7 @@ constexpr int kRunMaxLarge = 8;   // spheres per FK op when N > 128
 constexpr int kSaves = 2;         // saved branch-point FK frames (LDS, one column per waypoint)
 constexpr int kSumBlock = 64;     // canonical blocked summation over rollouts
 constexpr int kBandBatch = 8;     // rows per load batch of the noise band products
-constexpr int kMatPadRows = 12 * kBandBatch;  // zero rows past N in LT / MT (chunk + ring look-ahead)
+constexpr int kMatPadRows = 16 * kBandBatch;  // zero rows past N in LT / MT (ring look-ahead)
 constexpr int kVelTap0 = 2;       // non-zero taps of the velocity rule DIFF_RULES[0]
 constexpr int kVelTap1 = 5;       // (stomp_utils.h:54), checked in stomp_engine_create
 constexpr int kNoiseJT = 8;       // joints per tile of the rollout kernel's noise phase (2 x 4 per lane)

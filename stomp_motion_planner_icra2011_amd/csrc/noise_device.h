@@ -69,7 +69,10 @@ __device__ __forceinline__ void band_product(const double* __restrict__ AT, int 
 // three batches ahead; whole batches only (no branch between a batch's load and its use,
 // which would let the compiler sink the load to the use): the batch past kend adds exact
 // zeros (AT zero rows past N, kMatPadRows >= 4 * 4 * kBandK; v zero rows up to N + kBandBatch).
-constexpr int kBandK = 4;   // rows per batch
+#ifndef BAND_K
+#define BAND_K 4
+#endif
+constexpr int kBandK = BAND_K;   // rows per batch
 static_assert(kMatPadRows >= 4 * 4 * kBandK && kBandBatch >= kBandK, "band_tile padding");
 constexpr int kCtlRun = 4;  // padded indices per lane in the rollout kernel's control stencils
 template <int TI, int T0, int RT>
