@@ -4,9 +4,10 @@
  * are relative to /root/reference/stomp_motion_planner/.
  *
  * Floating-point contract: every sum is sequential in the index order the
- * reference's loops use, one rounding per operation (-ffp-contract=off), so the
- * dense ("reference structure") and banded/triangular evaluations agree bit for
- * bit (the skipped terms are exact zeros).  Sums over rollouts use a fixed
+ * reference's loops use, one rounding per operation (-ffp-contract=off), except the
+ * noise path's two dense products (L z, M eps), which round once per multiply-add
+ * (matvec_fma); the dense ("reference structure") and banded/triangular evaluations
+ * agree bit for bit (the skipped terms are exact zeros).  Sums over rollouts use a fixed
  * blocked order (blocks of cfg.sum_block consecutive rollouts, each summed
  * sequentially from 0.0, block partials then summed sequentially from 0.0);
  * for K <= sum_block this is exactly the reference's sequential order
@@ -729,6 +730,38 @@ static void control_costs(const so_problem* P, const double* params, const doubl
     }
 }
 
+/* The noise path's dense products (L z in MultivariateGaussian::sample and M eps in
+ * computeProjectedNoise): k ascending, one rounding per multiply-add (fma) -- the engine's
+ * contract for these two products, which it evaluates on the fp64 matrix cores (a
+ * v_mfma_f64_16x16x4_f64 chain is exactly this fma chain; tools/probes/mfma_f64_probe.hip).
+ * Hardware fma when the host has it, libm's correctly rounded fma otherwise (same bits). */
+__attribute__((target("fma"))) static void matvec_fma_hw(const double* A, int n, const double* x, double* y,
+                                                          int lower_only)
+{
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        int kend = lower_only ? i + 1 : n;
+        for (int k = 0; k < kend; ++k) s = __builtin_fma(A[(size_t)i * n + k], x[k], s);
+        y[i] = s;
+    }
+}
+
+static void matvec_fma(const double* A, int n, const double* x, double* y, int lower_only)
+{
+    static int hw = -1;
+    if (hw < 0) hw = __builtin_cpu_supports("fma") ? 1 : 0;
+    if (hw) {
+        matvec_fma_hw(A, n, x, y, lower_only);
+        return;
+    }
+    for (int i = 0; i < n; ++i) {
+        double s = 0.0;
+        int kend = lower_only ? i + 1 : n;
+        for (int k = 0; k < kend; ++k) s = fma(A[(size_t)i * n + k], x[k], s);
+        y[i] = s;
+    }
+}
+
 static void matvec(const double* A, int n, const double* x, double* y, int lower_only)
 {
     for (int i = 0; i < n; ++i) {
@@ -833,7 +866,7 @@ static void generate_rollouts(so_problem* P, int iteration_number, const double*
         for (int r = 0; r < P->K_gen; ++r) {
             so_normals(P->cfg.seed, iteration_number, d, r, N, z);
             /* MultivariateGaussian::sample: output = mean + L * z (multivariate_gaussian.h:88-94) */
-            matvec(P->L, N, z, tmp, !P->cfg.dense);
+            matvec_fma(P->L, N, z, tmp, !P->cfg.dense);
             double* nz = P->r_noise + r * JN + (size_t)d * N;
             double* pr = P->r_params + r * JN + (size_t)d * N;
             for (int t = 0; t < N; ++t) {
@@ -871,7 +904,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
     /* computeProjectedNoise for all K (policy_improvement.cpp:283-290, 473-482) */
     for (int r = 0; r < K; ++r)
         for (int d = 0; d < J; ++d)
-            matvec(P->M, N, P->r_noise + r * JN + (size_t)d * N, P->r_nproj + r * JN + (size_t)d * N, 0);
+            matvec_fma(P->M, N, P->r_noise + r * JN + (size_t)d * N, P->r_nproj + r * JN + (size_t)d * N, 0);
 
     /* Task::execute for each generated rollout (policy_improvement_loop.cpp:165-170) */
     int nthreads = P->cfg.threads > 0 ? P->cfg.threads : 1;
@@ -950,7 +983,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
         /* addExtraRollouts (policy_improvement.cpp:443-462) */
         memcpy(P->x_params, P->theta, JN * 8);
         for (size_t k = 0; k < JN; ++k) P->x_noise[k] = P->x_params[k] - P->theta[k];
-        for (int d = 0; d < J; ++d) matvec(P->M, N, P->x_noise + (size_t)d * N, P->x_nproj + (size_t)d * N, 0);
+        for (int d = 0; d < J; ++d) matvec_fma(P->M, N, P->x_noise + (size_t)d * N, P->x_nproj + (size_t)d * N, 0);
         double* xall = dalloc((size_t)Nall);
         double* call = dalloc((size_t)Nall);
         control_costs(P, P->x_params, P->x_nproj, 0.5 * P->cfg.smoothness_cost_weight, P->x_ctrl, xall, call);

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
             for (int t = 1; t < N; ++t) x += ct[(size_t)d * N + t];
             s += x;
         }
-        costs[c] = s;
+        costs[c] = s != s ? __builtin_inf() : s;   // NaN ranks last: the ranks stay a permutation
     }
     __syncthreads();
     for (int c = tid; c < n; c += bs) {

@@ -17,7 +17,8 @@
 
 namespace stomp {
 
-// acc[rr] += sum_{k < kend} AT[k][i] * v[k * vstride + rr], k ascending.  Unconditional loads
+// acc[rr] = fma(AT[k][i], v[k * vstride + rr], acc[rr]) for k < kend ascending (the noise
+// products' contract: one rounding per multiply-add, as on the matrix cores).  Unconditional loads
 // in four 8-load batches that rotate roles without register copies, so three batches are in
 // flight while one is summed (a copy of the next batch into the current one would make the
 // compiler wait for the batch it has just issued).  AT has kMatPadRows zero rows past N and v
@@ -39,7 +40,7 @@ __device__ __forceinline__ void band_product(const double* __restrict__ AT, int 
         for (int q = 0; q < P; ++q) {
             const double* x = v + (k0 + q) * vstride;
 #pragma unroll
-            for (int rr = 0; rr < RT; ++rr) acc[rr] += buf[q] * x[rr];
+            for (int rr = 0; rr < RT; ++rr) acc[rr] = __builtin_fma(buf[q], x[rr], acc[rr]);
         }
     };
     load(A0, 0);
@@ -192,11 +193,55 @@ __device__ __forceinline__ void rollout_normals(const NoiseArgs& a, int r, doubl
     }
 }
 
+// One 16 x 16 output tile of D = A * B on the fp64 matrix cores, k ascending from +0.0:
+// A[i][k] = AT[k][i0 + i] (rows past N read column N - 1 and are discarded), B[k][j] =
+// v[k * JP + j0 + j] (LDS, zero rows past N and zero columns past J).  Lane l supplies
+// A[l & 15][k + (l >> 4)] and B[k + (l >> 4)][l & 15] for each 4-deep k step and holds
+// D[(l >> 4) + 4 r][l & 15] (r < 4).  Each v_mfma_f64_16x16x4_f64 is a k-ascending fma
+// chain (tools/probes/mfma_f64_probe.hip), so D is the oracle's matvec_fma bit for bit.
+// Operands go out eight k steps at a time, double buffered.
+typedef double d4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ d4_t mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, int i0, int kend, const double* v,
+                                          int JP, int j0, int lane)
+{
+    constexpr int S = 8;   // k steps per batch
+    const int li = lane & 15, lk = lane >> 4;
+    // lane part of the address (column, row within the step) in the VGPR offset, the step's
+    // rows in the scalar offset (a lane-dependent scalar offset would become a waterfall loop)
+    const int ioff = (min(i0 + li, N - 1) + lk * N) * (int)sizeof(double);
+    const double* vb = v + lk * JP + j0 + li;
+    d4_t acc = {0.0, 0.0, 0.0, 0.0};
+    const int nsteps = (kend + 3) >> 2;
+    double a0[S], b0[S], a1[S], b1[S];
+    auto load = [&](double* a, double* b, int s0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k4 = 4 * min(s0 + s, nsteps - 1);   // clamped: the tail re-reads a valid step
+            a[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, ioff, k4 * N * (int)sizeof(double), 0));
+            b[s] = vb[k4 * JP];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto run = [&](const double* a, const double* b, int s0) {
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (s0 + s < nsteps) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+    };
+    load(a0, b0, 0);
+    for (int s0 = 0; s0 < nsteps; s0 += 2 * S) {
+        load(a1, b1, s0 + S);
+        run(a0, b0, s0);
+        if (s0 + S >= nsteps) break;
+        load(a0, b0, s0 + 2 * S);
+        run(a1, b1, s0 + S);
+    }
+    return acc;
+}
+
 template <int BLOCK>
 __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                 int tid)
 {
-    constexpr int RT = 4;   // joints per lane
     const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J);
     const size_t row = (size_t)r * J * N;
     const double* zs = zA;
@@ -204,49 +249,56 @@ __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, doubl
     __syncthreads();   // the normals are complete
     STAMP(7);
 
-    // Lane l of wave w owns waypoint i = 32 w + (l & 31) and joints h * 4 .. h * 4 + 3 of each
-    // 8-joint tile (h = l >> 5): a matrix row's element is loaded once per workgroup, not once
-    // per joint tile, which is what bounds this phase (L2 -> CU bandwidth), and each load
-    // feeds four products.
-    const int wv = tid >> 6, lane = tid & 63;
-    const int i = 32 * wv + (lane & 31), h = lane >> 5;
-    int col[1] = {min(i, N - 1)};
-    const int ntile = JP / kNoiseJT;
-    // L is lower triangular: the wave's waypoints need rows k < 32 w + 32 only
-    const int lz_end = min(N, 32 * wv + 32);
-    for (int tl = 0; tl < ntile; ++tl) {
-        const int d0 = tl * kNoiseJT + h * RT;
-        double acc[1][RT];
+    constexpr int NW = BLOCK / 64;
+    // the wave index through readfirstlane: the compiler then knows every tile quantity is
+    // wave-uniform (scalar buffer offsets; a "divergent" one becomes a waterfall loop)
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    const int nti = (N + 15) >> 4, ntj = JP >> 4, ntiles = nti * ntj;
+    const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
+    const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)a.LT, 0, mat_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
+    // waypoint tiles in snake order over the waves (L z costs grow with the tile index);
+    // a permutation of [0, ntiles): odd rounds run backwards over the tiles they have
+    auto tile_of = [&](int n) {
+        const int round = n / NW, pos = n % NW, cnt = min(NW, ntiles - round * NW);
+        return round * NW + ((round & 1) ? cnt - 1 - pos : pos);
+    };
+    // eps = sigma_d * (0 + L z): L is lower triangular, tile ti needs rows k < 16 ti + 16
+    for (int n = wv; n < ntiles; n += NW) {
+        const int tt = tile_of(n);
+        const int ti = tt % nti, tj = tt / nti;
+        const d4_t acc = mfma_tile(rL, N, 16 * ti, min(N, 16 * ti + 16), zs, JP, 16 * tj, lane);
+        const int d = 16 * tj + li;
 #pragma unroll
-        for (int rr = 0; rr < RT; ++rr) acc[0][rr] = 0.0;
-        band_tile<1, 0, RT>(a.LT, N, col, 0, lz_end, zs + d0, JP, acc);
-#pragma unroll
-        for (int rr = 0; rr < RT; ++rr) {
-            const int d = d0 + rr;
-            if (d >= J || i >= N) continue;
-            const double e = a.sigma.v[d] * (0.0 + acc[0][rr]);
-            const double p = a.theta[(size_t)d * N + i] + e;
-            a.noise[row + (size_t)d * N + i] = e;
-            a.params[row + (size_t)d * N + i] = p;
-            traj[d * N + i] = p;
-            eps[i * JP + d] = e;
+        for (int q = 0; q < 4; ++q) {
+            const int i = 16 * ti + lk + 4 * q;
+            if (i < N && d < J) {
+                const double e = a.sigma.v[d] * (0.0 + acc[q]);
+                traj[d * N + i] = a.theta[(size_t)d * N + i] + e;
+                eps[i * JP + d] = e;
+            }
         }
     }
     __syncthreads();
 
     STAMP(8);
+    // the rows to HBM, coalesced (lane over waypoints)
+    for (int idx = tid; idx < J * N; idx += BLOCK) {
+        const int d = idx / N, i = idx - d * N;
+        a.noise[row + idx] = eps[i * JP + d];
+        a.params[row + idx] = traj[idx];
+    }
     double* xs = zA;   // z is dead
-    for (int tl = 0; tl < ntile; ++tl) {
-        const int d0 = tl * kNoiseJT + h * RT;
-        double acc[1][RT];
+    // x = params + M eps
+    for (int n = wv; n < ntiles; n += NW) {
+        const int ti = n % nti, tj = n / nti;
+        const d4_t acc = mfma_tile(rM, N, 16 * ti, N, eps, JP, 16 * tj, lane);
+        const int d = 16 * tj + li;
 #pragma unroll
-        for (int rr = 0; rr < RT; ++rr) acc[0][rr] = 0.0;
-        band_tile<1, 0, RT>(a.MT, N, col, 0, N, eps + d0, JP, acc);
-#pragma unroll
-        for (int rr = 0; rr < RT; ++rr) {
-            const int d = d0 + rr;
-            if (d >= J || i >= N) continue;
-            xs[d * Nall + i + 6] = traj[d * N + i] + acc[0][rr];
+        for (int q = 0; q < 4; ++q) {
+            const int i = 16 * ti + lk + 4 * q;
+            if (i < N && d < J) xs[d * Nall + i + 6] = traj[d * N + i] + acc[q];
         }
     }
     for (int idx = tid; idx < J * 12; idx += BLOCK) {
