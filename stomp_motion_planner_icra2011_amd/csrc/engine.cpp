@@ -326,7 +326,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
     const int num_gen = std::max(g1 - g0, 0);
 #ifndef STOMP_SEPARATE_NOISE
-    const bool fused = e->N <= 128;   // rollout_project's register tiling covers 128 waypoints
+    const bool fused = e->J <= 16;   // rollout_project: at most four 4-joint column groups
 #else
     const bool fused = false;
 #endif

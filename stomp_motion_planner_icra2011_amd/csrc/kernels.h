@@ -26,7 +26,7 @@ constexpr int kBandBatch = 8;     // rows per load batch of the noise band produ
 constexpr int kMatPadRows = 16 * kBandBatch;  // zero rows past N in LT / MT (ring look-ahead)
 constexpr int kVelTap0 = 2;       // non-zero taps of the velocity rule DIFF_RULES[0]
 constexpr int kVelTap1 = 5;       // (stomp_utils.h:54), checked in stomp_engine_create
-constexpr int kNoiseJT = 16;      // joint columns per matrix-core tile of the rollout kernel's noise phase
+constexpr int kNoiseJT = 4;       // joint columns per matrix-core block of the rollout kernel's noise phase
 
 inline int run_max(int N) { return N <= 128 ? kRunMaxSmall : kRunMaxLarge; }
 

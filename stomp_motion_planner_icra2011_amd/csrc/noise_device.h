@@ -193,54 +193,71 @@ __device__ __forceinline__ void rollout_normals(const NoiseArgs& a, int r, doubl
     }
 }
 
-// One 16 x 16 output tile of D = A * B on the fp64 matrix cores, k ascending from +0.0:
-// A[i][k] = AT[k][i0 + i] (rows past N read column N - 1 and are discarded), B[k][j] =
-// v[k * JP + j0 + j] (LDS, zero rows past N and zero columns past J).  Lane l supplies
-// A[l & 15][k + (l >> 4)] and B[k + (l >> 4)][l & 15] for each 4-deep k step and holds
-// D[(l >> 4) + 4 r][l & 15] (r < 4).  Each v_mfma_f64_16x16x4_f64 is a k-ascending fma
-// chain (tools/probes/mfma_f64_probe.hip), so D is the oracle's matvec_fma bit for bit.
-// Operands go out eight k steps at a time, double buffered.
-typedef double d4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ d4_t mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, int i0, int kend, const double* v,
-                                          int JP, int j0, int lane)
+// One 16-row tile of D = A * B on the fp64 matrix cores, k ascending from +0.0, for NG groups
+// of 4 joint columns: A[i][k] = AT[k][i0 + i] (rows past N read column N - 1 and are
+// discarded), B[k][j] = v[k * JP + 4 g + j] (LDS; zero rows past N, zero columns past J).
+// v_mfma_f64_4x4x4_4b_f64 computes four 4 x 4 blocks b = lane bits 2-3: A_b[i][k] at lane
+// 16 k + 4 b + i, B_b[k][j] at 16 k + 4 b + j, D_b[i][j] at 16 i + 4 b + j
+// (tools/probes/mfma_f64_4x4_map.hip).  With block b = rows 4 b .. 4 b + 3 of the tile and B
+// the same in every block, one instruction advances a 16 x 4 tile by 4 k, and it is a
+// k-ascending fma chain (tools/probes/mfma_f64_4x4_probe.hip): D is the oracle's matvec_fma
+// bit for bit.  The NG column groups share the A operand and are independent chains.
+// Lane l ends with D[4 ((l >> 2) & 3) + (l >> 4)][4 g + (l & 3)] in acc[g].
+template <int NG>
+__device__ __forceinline__ void mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, int i0, int kend, const double* v,
+                                          int JP, int lane, double* acc)
 {
-    constexpr int S = 8;   // k steps per batch
-    const int li = lane & 15, lk = lane >> 4;
+    constexpr int S = 8 / NG;   // k steps per batch; four batches rotate, three ahead of the MFMAs
+    const int lk = lane >> 4;
     // lane part of the address (column, row within the step) in the VGPR offset, the step's
     // rows in the scalar offset (a lane-dependent scalar offset would become a waterfall loop)
-    const int ioff = (min(i0 + li, N - 1) + lk * N) * (int)sizeof(double);
-    const double* vb = v + lk * JP + j0 + li;
-    d4_t acc = {0.0, 0.0, 0.0, 0.0};
+    const int ioff = (min(i0 + (lane & 15), N - 1) + lk * N) * (int)sizeof(double);
+    const double* vb = v + lk * JP + (lane & 3);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = 0.0;
     const int nsteps = (kend + 3) >> 2;
-    double a0[S], b0[S], a1[S], b1[S];
-    auto load = [&](double* a, double* b, int s0) {
+    const int nb = (nsteps + S - 1) / S;
+    struct Batch {
+        double a[S], b[S][NG];
+    };
+    Batch R0, R1, R2, R3;
+    auto load = [&](Batch& R, int bi) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const int k4 = 4 * min(s0 + s, nsteps - 1);   // clamped: the tail re-reads a valid step
-            a[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, ioff, k4 * N * (int)sizeof(double), 0));
-            b[s] = vb[k4 * JP];
+            const int k4 = 4 * min(bi * S + s, nsteps - 1);   // clamped: batches past the end re-read
+            R.a[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, ioff, k4 * N * (int)sizeof(double), 0));
+#pragma unroll
+            for (int g = 0; g < NG; ++g) R.b[s][g] = vb[k4 * JP + 4 * g];
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto run = [&](const double* a, const double* b, int s0) {
+    auto run = [&](const Batch& R, int bi) {
 #pragma unroll
         for (int s = 0; s < S; ++s)
-            if (s0 + s < nsteps) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+            if (bi * S + s < nsteps)
+#pragma unroll
+                for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f64_4x4x4f64(R.a[s], R.b[s][g], acc[g], 0, 0, 0);
     };
-    load(a0, b0, 0);
-    for (int s0 = 0; s0 < nsteps; s0 += 2 * S) {
-        load(a1, b1, s0 + S);
-        run(a0, b0, s0);
-        if (s0 + S >= nsteps) break;
-        load(a0, b0, s0 + 2 * S);
-        run(a1, b1, s0 + S);
+    // whole ring rounds, then the remaining batches (no branch between a load and its use)
+    load(R0, 0);
+    load(R1, 1);
+    load(R2, 2);
+    int bi = 0;
+    for (; bi + 4 <= nb; bi += 4) {
+        load(R3, bi + 3); run(R0, bi);
+        load(R0, bi + 4); run(R1, bi + 1);
+        load(R1, bi + 5); run(R2, bi + 2);
+        load(R2, bi + 6); run(R3, bi + 3);
     }
-    return acc;
+    const int rem = nb - bi;
+    if (rem >= 1) run(R0, bi);
+    if (rem >= 2) run(R1, bi + 1);
+    if (rem >= 3) run(R2, bi + 2);
 }
 
-template <int BLOCK>
-__device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
-                                                int tid)
+template <int BLOCK, int NG>
+__device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
+                                                   int tid)
 {
     const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J);
     const size_t row = (size_t)r * J * N;
@@ -253,28 +270,28 @@ __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, doubl
     // the wave index through readfirstlane: the compiler then knows every tile quantity is
     // wave-uniform (scalar buffer offsets; a "divergent" one becomes a waterfall loop)
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int li = lane & 15, lk = lane >> 4;
-    const int nti = (N + 15) >> 4, ntj = JP >> 4, ntiles = nti * ntj;
+    const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;   // lane's D element
+    const int nti = (N + 15) >> 4;
     const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
     const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)a.LT, 0, mat_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
     // waypoint tiles in snake order over the waves (L z costs grow with the tile index);
-    // a permutation of [0, ntiles): odd rounds run backwards over the tiles they have
+    // a permutation of [0, nti): odd rounds run backwards over the tiles they have
     auto tile_of = [&](int n) {
-        const int round = n / NW, pos = n % NW, cnt = min(NW, ntiles - round * NW);
+        const int round = n / NW, pos = n % NW, cnt = min(NW, nti - round * NW);
         return round * NW + ((round & 1) ? cnt - 1 - pos : pos);
     };
     // eps = sigma_d * (0 + L z): L is lower triangular, tile ti needs rows k < 16 ti + 16
-    for (int n = wv; n < ntiles; n += NW) {
-        const int tt = tile_of(n);
-        const int ti = tt % nti, tj = tt / nti;
-        const d4_t acc = mfma_tile(rL, N, 16 * ti, min(N, 16 * ti + 16), zs, JP, 16 * tj, lane);
-        const int d = 16 * tj + li;
+    for (int n = wv; n < nti; n += NW) {
+        const int ti = tile_of(n);
+        double acc[NG];
+        mfma_tile<NG>(rL, N, 16 * ti, min(N, 16 * ti + 16), zs, JP, lane, acc);
+        const int i = 16 * ti + irow;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = 16 * ti + lk + 4 * q;
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
             if (i < N && d < J) {
-                const double e = a.sigma.v[d] * (0.0 + acc[q]);
+                const double e = a.sigma.v[d] * (0.0 + acc[g]);
                 traj[d * N + i] = a.theta[(size_t)d * N + i] + e;
                 eps[i * JP + d] = e;
             }
@@ -291,14 +308,14 @@ __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, doubl
     }
     double* xs = zA;   // z is dead
     // x = params + M eps
-    for (int n = wv; n < ntiles; n += NW) {
-        const int ti = n % nti, tj = n / nti;
-        const d4_t acc = mfma_tile(rM, N, 16 * ti, N, eps, JP, 16 * tj, lane);
-        const int d = 16 * tj + li;
+    for (int ti = wv; ti < nti; ti += NW) {
+        double acc[NG];
+        mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
+        const int i = 16 * ti + irow;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = 16 * ti + lk + 4 * q;
-            if (i < N && d < J) xs[d * Nall + i + 6] = traj[d * N + i] + acc[q];
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
+            if (i < N && d < J) xs[d * Nall + i + 6] = traj[d * N + i] + acc[g];
         }
     }
     for (int idx = tid; idx < J * 12; idx += BLOCK) {
@@ -352,6 +369,15 @@ __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, doubl
         }
     }
     STAMP(63);
+}
+
+// the engine runs the fused phase for J <= 16 (at most four groups of 4 joint columns)
+template <int BLOCK>
+__device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
+                                                int tid)
+{
+    if (a.J <= 8) rollout_project_ng<BLOCK, 2>(a, r, traj, zA, zB, tid);
+    else rollout_project_ng<BLOCK, 4>(a, r, traj, zA, zB, tid);
 }
 
 }  // namespace stomp
