@@ -222,7 +222,15 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     STAMP(3);
 
     // ---- FK program, slot by slot, with the slot's pairs in between
-    const int t_own = tid;                      // FK / fold lane: waypoint tid (tid < N)
+    // FK / fold lane: waypoint t_own (< N).  Odd workgroups run the FK program on waves 2-3
+    // (N <= 128): two workgroups share a CU, and their waves 0-1 would otherwise share SIMDs
+    // while the FK-idle waves leave the other two SIMDs empty
+#ifndef FK_NO_SPREAD
+    const int t_own = tid - ((N <= 128 && (e & 1)) ? 128 : 0);
+#else
+    const int t_own = tid;
+#endif
+    const bool fk_lane = t_own >= 0 && t_own < N;
     const int G = BLOCK / N, pg = tid / N, pt = tid - pg * N;   // pair lanes: (group, waypoint)
     // C: running frame in the registers of lanes t < N; branch-point frames saved in LDS
     // (column t of sv).  Lanes t < N are also pair lanes (0, t).
@@ -231,7 +239,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     bool col = false;
     // one FK program step (stomp_optimizer.cpp via treefksolverjointposaxis_partial.cpp:108-140)
     auto fk_op = [&](const FkOp& o) {
-        if (o.seg < 0 || t_own >= N) return;
+        if (o.seg < 0 || !fk_lane) return;
         const DevSegment& sg = seg_s[o.seg];
         double st = 0.0, ct = 1.0;
         if (sg.q_index >= 0) det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
@@ -271,7 +279,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     int op = fk_advance(0);
     while (op < m.nops) {
         const FkOp o = ops_s[op];
-        if (t_own < N) {
+        if (fk_lane) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) fb[k * N + t_own] = C.R[k];
 #pragma unroll
@@ -344,7 +352,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
 #ifndef FK_PIPELINE
         // C is reloaded from fb (not kept live across the pairs)
-        if (t_own < N) {
+        if (fk_lane) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
 #pragma unroll
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 #endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * o.slot);
-        if (t_own < N) {
+        if (fk_lane) {
             // fold in sphere order; the LDS reads go out 16 at a time
             const int nsl = se - sb;
             for (int q0 = 0; q0 < nsl; q0 += 16) {
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     STAMP(4);
     if (col) flag = 1;   // every writer stores 1
     __syncthreads();     // folds done (av reused below), flag complete
-    if (t_own < N) {
+    if (fk_lane) {
         const double cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
         double* so = extra ? a.x_state : a.state_out + (long long)e * N;
         so[t_own] = cost;
