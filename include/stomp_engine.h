@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define STOMP_ENGINE_ABI_VERSION 1
+#define STOMP_ENGINE_ABI_VERSION 2
 
 #define STOMP_OK 0
 #define STOMP_E_INVALID (-1)   /* bad sizes / arguments */
@@ -89,6 +89,27 @@ typedef struct stomp_grid {
     int32_t data_on_device;     /* 1: engine uses the buffer in place (caller keeps it alive) */
 } stomp_grid;
 
+/* KDL::RigidBodyInertia(m, cog, Ic) of a segment, in the segment frame; Ic about the
+ * centre of mass as (Ixx, Iyy, Izz, Ixy, Ixz, Iyz).  Replaces the URDF <inertial> data
+ * KDL's ChainIdSolver_RNE reads (stomp_robot_model.cpp:185-189). */
+typedef struct stomp_inertia {
+    double mass;
+    double com[3];
+    double inertia[6];
+} stomp_inertia;
+
+/* motion_planning_msgs::OrientationConstraint as OrientationConstraintEvaluator stores it
+ * (constraint_evaluator.cpp:50-73) */
+typedef struct stomp_orientation_constraint {
+    int32_t segment;            /* frame_number_ = segmentNameToIndex(link_name) */
+    double orientation[4];      /* nominal orientation quaternion (x, y, z, w) */
+    int32_t body_fixed;         /* 0: type == HEADER_FRAME, 1: body-fixed */
+    double absolute_roll_tolerance;
+    double absolute_pitch_tolerance;
+    double absolute_yaw_tolerance;
+    double weight;
+} stomp_orientation_constraint;
+
 typedef struct stomp_engine_desc {
     int32_t abi_version;        /* STOMP_ENGINE_ABI_VERSION */
     int32_t num_joints;         /* J (planning group joints) */
@@ -107,7 +128,7 @@ typedef struct stomp_engine_desc {
     double smoothness_cost_weight;
     double obstacle_cost_weight;
     double constraint_cost_weight;
-    double torque_cost_weight;  /* > 1e-9 -> STOMP_E_UNSUPPORTED (torque term not built yet) */
+    double torque_cost_weight;  /* > 1e-9: torque term (stomp_optimizer.cpp:1117-1142) */
     const double* noise_stddev; /* J */
     const double* noise_decay;  /* J */
     int32_t use_cumulative_costs;
@@ -121,6 +142,16 @@ typedef struct stomp_engine_desc {
     int32_t rank;               /* rollout shard of this process (0 if world_size == 1) */
     int32_t world_size;         /* processes sharing the K rollouts (1 = no collectives) */
     const void* comm_id;        /* 128-byte RCCL unique id from stomp_comm_unique_id (rank 0) */
+    /* torque term: inverse dynamics over the chain torque_root (exclusive) -> torque_tip
+     * (inclusive), whose joints must be the group's joints in order (the reference's
+     * kdl_tree_.getChain("torso_lift_link", "r_gripper_tool_frame"), stomp_robot_model.cpp:185-189) */
+    const stomp_inertia* inertias;  /* num_segments; may be NULL while the torque term is off */
+    int32_t torque_root;
+    int32_t torque_tip;
+    double gravity[3];              /* in the torque_root frame (the reference: 0, 0, -9.8) */
+    /* orientation path constraints (stomp_optimizer.cpp:195-201, 1107-1115) */
+    int32_t num_orientation_constraints;
+    const stomp_orientation_constraint* orientation_constraints;
 } stomp_engine_desc;
 
 typedef struct stomp_engine stomp_engine;

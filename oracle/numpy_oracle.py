@@ -175,3 +175,55 @@ class NumpyStomp:
         cost, cf, traj = self.execute(self.theta, it - 1)
         return dict(noise=noise, params=params, nproj=nproj, state=state, control=ctrl, prob=P,
                     cost=float(cost.sum()), collision_free=cf, traj=traj)
+
+
+def inverse_dynamics(problem, q, qd, qdd):
+    """Independent restatement of the torque term's inverse dynamics (the role of
+    KDL::ChainIdSolver_RNE, stomp_robot_model.cpp:185-189, stomp_optimizer.cpp:1049-1053) in
+    the classical world-frame form (Luh-Walker-Paul / Craig): every quantity in the chain-root
+    frame, 3-vectors only, numpy libm trigonometry.  Shares nothing with the C oracle's
+    spatial-algebra sweep; the two agree to rounding."""
+    p = problem
+    chain = p.torque_chain()
+    segs = [p.robot.segments[i] for i in chain]
+    R, o = np.eye(3), np.zeros(3)
+    w, dw = np.zeros(3), np.zeros(3)
+    acc = -np.array(p.gravity, np.float64)   # origin acceleration of the root frame
+    rec = []
+    for s in segs:
+        Rl = np.array(s.rot, np.float64).reshape(3, 3)
+        z = np.zeros(3)
+        qv = qdv = qddv = 0.0
+        if s.q_index >= 0:
+            qv, qdv, qddv = q[s.q_index], qd[s.q_index], qdd[s.q_index]
+            Rl = Rl @ pb.rot2(s.axis, qv)
+        o_new = R @ np.array(s.trans, np.float64) + o
+        d = o_new - o
+        acc = acc + np.cross(dw, d) + np.cross(w, np.cross(w, d))   # the joint sits at o_new
+        R = R @ Rl
+        if s.q_index >= 0:
+            z = R @ np.array(s.axis, np.float64)
+        w_new = w + z * qdv
+        dw = dw + z * qddv + np.cross(w_new, z * qdv)
+        w, o = w_new, o_new
+        inert = s.inertia
+        m = inert.mass if inert else 0.0
+        c = np.array(inert.com if inert else (0.0, 0.0, 0.0), np.float64)
+        iv = inert.inertia if inert else (0.0,) * 6
+        Ic = np.array([[iv[0], iv[3], iv[4]], [iv[3], iv[1], iv[5]], [iv[4], iv[5], iv[2]]])
+        r = R @ c
+        ac = acc + np.cross(dw, r) + np.cross(w, np.cross(w, r))
+        Iw = R @ Ic @ R.T
+        F = m * ac
+        Nm = Iw @ dw + np.cross(w, Iw @ w)
+        rec.append((s.q_index, z, o.copy(), r, F, Nm))
+    tau = np.zeros(p.J)
+    f, n, o_next = np.zeros(3), np.zeros(3), None
+    for qi, z, oi, r, F, Nm in reversed(rec):
+        arm = (o_next - oi) if o_next is not None else np.zeros(3)
+        n = Nm + n + np.cross(r, F) + np.cross(arm, f)
+        f = F + f
+        o_next = oi
+        if qi >= 0:
+            tau[qi] = z @ n
+    return tau

@@ -33,6 +33,16 @@ class so_sdf(C.Structure):
                 ("resolution", C.c_double), ("data", C.POINTER(C.c_float))]
 
 
+class so_inertia(C.Structure):
+    _fields_ = [("mass", C.c_double), ("com", C.c_double * 3), ("inertia", C.c_double * 6)]
+
+
+class so_orientation_constraint(C.Structure):
+    _fields_ = [("segment", C.c_int), ("orientation", C.c_double * 4), ("body_fixed", C.c_int),
+                ("absolute_roll_tolerance", C.c_double), ("absolute_pitch_tolerance", C.c_double),
+                ("absolute_yaw_tolerance", C.c_double), ("weight", C.c_double)]
+
+
 class so_config(C.Structure):
     _fields_ = [("num_joints", C.c_int), ("num_time_steps", C.c_int), ("num_rollouts", C.c_int),
                 ("num_reused_rollouts", C.c_int), ("num_segments", C.c_int),
@@ -45,7 +55,10 @@ class so_config(C.Structure):
                 ("noise_decay", C.POINTER(C.c_double)), ("use_cumulative_costs", C.c_int),
                 ("start", C.POINTER(C.c_double)), ("goal", C.POINTER(C.c_double)), ("seed", C.c_uint64),
                 ("max_iterations", C.c_int), ("max_iterations_after_collision_free", C.c_int),
-                ("sum_block", C.c_int), ("dense", C.c_int), ("threads", C.c_int)]
+                ("sum_block", C.c_int), ("dense", C.c_int), ("threads", C.c_int),
+                ("inertias", C.POINTER(so_inertia)), ("torque_root", C.c_int), ("torque_tip", C.c_int),
+                ("gravity", C.c_double * 3), ("num_orientation_constraints", C.c_int),
+                ("orientation_constraints", C.POINTER(so_orientation_constraint))]
 
 
 class so_iter_out(C.Structure):
@@ -94,6 +107,7 @@ def lib():
         l.so_sdf_distance.restype = C.c_double
         l.so_sdf_distance.argtypes = [P, C.c_double, C.c_double, C.c_double]
         l.so_potential.argtypes = [P, C.c_int, dp, dp]
+        l.so_inverse_dynamics.argtypes = [P, dp, dp, dp, dp]
         _lib = l
     return _lib
 
@@ -160,6 +174,19 @@ class Oracle:
         cfg.sum_block = sum_block
         cfg.dense = int(dense)
         cfg.threads = threads
+        self._inertia = _arr([so_inertia(s.inertia.mass, (C.c_double * 3)(*s.inertia.com),
+                                         (C.c_double * 6)(*s.inertia.inertia)) if s.inertia else so_inertia()
+                              for s in p.robot.segments], so_inertia)
+        cfg.inertias = self._inertia
+        cfg.torque_root = p.robot.index(p.torque_root)
+        cfg.torque_tip = p.robot.index(p.torque_tip)
+        cfg.gravity = (C.c_double * 3)(*p.gravity)
+        self._oc = _arr([so_orientation_constraint(p.robot.index(c.link_name), (C.c_double * 4)(*c.orientation),
+                                                   0 if c.header_frame else 1, c.absolute_roll_tolerance,
+                                                   c.absolute_pitch_tolerance, c.absolute_yaw_tolerance, c.weight)
+                         for c in p.orientation_constraints], so_orientation_constraint)
+        cfg.num_orientation_constraints = len(p.orientation_constraints)
+        cfg.orientation_constraints = self._oc
         self._cfg = cfg
         self.h = L.so_create(C.byref(cfg))
         if not self.h:
@@ -233,6 +260,13 @@ class Oracle:
         out = np.zeros((self.S, 3))
         lib().so_sphere_positions(self.h, _dp(qq), _dp(out))
         return out
+
+    def inverse_dynamics(self, q, qd, qdd) -> np.ndarray:
+        a = [np.ascontiguousarray(v, np.float64) for v in (q, qd, qdd)]
+        tau = np.zeros(self.J)
+        if lib().so_inverse_dynamics(self.h, _dp(a[0]), _dp(a[1]), _dp(a[2]), _dp(tau)) != 0:
+            raise RuntimeError("torque term off")
+        return tau
 
     def sdf_distance(self, x, y, z) -> float:
         return lib().so_sdf_distance(self.h, x, y, z)

@@ -62,6 +62,12 @@ struct so_problem {
     double last_cost;
     int last_cf;
     double* best_traj;     /* J x N */
+    /* torque term: chain segments root side first, their rigid-body inertias */
+    int torque, nchain;
+    int* chain;
+    double* rb_m;          /* nchain */
+    double* rb_h;          /* nchain x 3: m c */
+    double* rb_I;          /* nchain x 9: rotational inertia about the segment origin */
 };
 
 /* ---------------------------------------------------------------- linear algebra */
@@ -125,6 +131,8 @@ static void gram(const double* D, int n, double* G)
  * Build-defined replacement for boost::mt19937 + normal_distribution seeded with
  * rand() (multivariate_gaussian.h:83-94): Philox4x32-10 keyed by the problem
  * seed, counter (pair index, rollout, joint, iteration), Box-Muller. */
+#define SO_MAX_J 32
+#define SO_MAX_CHAIN 64
 #define PHILOX_M0 0xD2511F53u
 #define PHILOX_M1 0xCD9E8D57u
 #define PHILOX_W0 0x9E3779B9u
@@ -247,6 +255,193 @@ static void fk_spheres(const so_problem* P, const double* q, frame_t* frames, do
         frame_apply(&frames[P->sph[j].segment], P->sph[j].pos, pos + 3 * j);
 }
 
+/* ---------------------------------------------------------------- inverse dynamics
+ * KDL::ChainIdSolver_RNE::CartToJnt (orocos KDL, 3rd party, not vendored; constructed at
+ * stomp_robot_model.cpp:185-189, called from StompOptimizer::getTorques
+ * stomp_optimizer.cpp:1049-1053).  Restated from KDL's published recursion: outward sweep
+ * v_i = X_i^-1 v_{i-1} + S_i qd_i, a_i = X_i^-1 a_{i-1} + S_i qdd_i + v_i x (S_i qd_i) (root:
+ * a_0 = X_0^-1 (-gravity, 0)), f_i = I_i a_i + v_i x* (I_i v_i); inward sweep tau_i = S_i . f_i,
+ * f_{i-1} += X_i f_i.  Twists / wrenches are (linear, angular) in segment coordinates with the
+ * KDL Frame/Twist/Wrench/RigidBodyInertia operators below.  In this build's segment
+ * convention the segment frame sits on its joint axis, so the unit twist is S = (0, axis).
+ * PARITY UNPINNED against KDL (no KDL in the container). */
+typedef struct { double vel[3]; double rot[3]; } twist_t;
+typedef struct { double force[3]; double torque[3]; } wrench_t;
+
+static void v_cross(const double* a, const double* b, double* c)   /* KDL Vector * Vector */
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+static void rot_mul_v(const double* R, const double* v, double* o)   /* Rotation * Vector */
+{
+    for (int i = 0; i < 3; ++i) o[i] = R[3 * i + 0] * v[0] + R[3 * i + 1] * v[1] + R[3 * i + 2] * v[2];
+}
+
+static void rot_inv_mul_v(const double* R, const double* v, double* o)   /* Rotation::Inverse(Vector) */
+{
+    for (int i = 0; i < 3; ++i) o[i] = R[0 + i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
+}
+
+/* Frame::Inverse(Twist): (R^T (v - p x w), R^T w) */
+static void frame_inv_twist(const double* R, const double* p, const twist_t* t, twist_t* o)
+{
+    double pw[3], d[3];
+    v_cross(p, t->rot, pw);
+    for (int k = 0; k < 3; ++k) d[k] = t->vel[k] - pw[k];
+    rot_inv_mul_v(R, d, o->vel);
+    rot_inv_mul_v(R, t->rot, o->rot);
+}
+
+/* Twist * Twist (motion cross product): (a.w x b.v + a.v x b.w, a.w x b.w) */
+static void twist_cross(const twist_t* a, const twist_t* b, twist_t* o)
+{
+    double x[3], y[3];
+    v_cross(a->rot, b->vel, x);
+    v_cross(a->vel, b->rot, y);
+    for (int k = 0; k < 3; ++k) o->vel[k] = x[k] + y[k];
+    v_cross(a->rot, b->rot, o->rot);
+}
+
+/* RigidBodyInertia * Twist: (m v - h x w, I w + h x v) */
+static void rbi_mul(double m, const double* h, const double* I, const twist_t* t, wrench_t* o)
+{
+    double hw[3], hv[3], Iw[3];
+    v_cross(h, t->rot, hw);
+    v_cross(h, t->vel, hv);
+    rot_mul_v(I, t->rot, Iw);
+    for (int k = 0; k < 3; ++k) {
+        o->force[k] = m * t->vel[k] - hw[k];
+        o->torque[k] = Iw[k] + hv[k];
+    }
+}
+
+/* Twist * Wrench (force cross product): (w x f, w x n + v x f) */
+static void twist_cross_wrench(const twist_t* t, const wrench_t* w, wrench_t* o)
+{
+    double a[3], b[3];
+    v_cross(t->rot, w->force, o->force);
+    v_cross(t->rot, w->torque, a);
+    v_cross(t->vel, w->force, b);
+    for (int k = 0; k < 3; ++k) o->torque[k] = a[k] + b[k];
+}
+
+/* Frame * Wrench: (R f, R n + p x (R f)) */
+static void frame_wrench(const double* R, const double* p, const wrench_t* w, wrench_t* o)
+{
+    double rn[3], pf[3];
+    rot_mul_v(R, w->force, o->force);
+    rot_mul_v(R, w->torque, rn);
+    v_cross(p, o->force, pf);
+    for (int k = 0; k < 3; ++k) o->torque[k] = rn[k] + pf[k];
+}
+
+/* KDL::RigidBodyInertia(m, c, Ic): h = m c, I = Ic - m (c c^T - (c.c) 1) */
+static void rb_inertia(const so_inertia* in, double* m, double* h, double* I)
+{
+    const double* c = in->com;
+    const double* v = in->inertia;
+    const double Ic[9] = {v[0], v[3], v[4], v[3], v[1], v[5], v[4], v[5], v[2]};
+    const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+    *m = in->mass;
+    for (int i = 0; i < 3; ++i) {
+        h[i] = in->mass * c[i];
+        for (int j = 0; j < 3; ++j) I[3 * i + j] = Ic[3 * i + j] - in->mass * (c[i] * c[j] - (i == j ? cc : 0.0));
+    }
+}
+
+int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, const double* qdd, double* tau)
+{
+    if (!P->torque) return -1;
+    wrench_t f[64];
+    double Rs[64][9];
+    const double* g = P->cfg.gravity;
+    const twist_t ag = {{-g[0], -g[1], -g[2]}, {0.0, 0.0, 0.0}};
+    twist_t v = {{0}}, a = {{0}};
+    for (int i = 0; i < P->nchain; ++i) {
+        const so_segment* sg = &P->segs[P->chain[i]];
+        const int j = sg->q_index;
+        double qv = 0.0, qdv = 0.0, qddv = 0.0;
+        twist_t S = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+        if (j >= 0) {
+            qv = q[j]; qdv = qd[j]; qddv = qdd[j];
+            for (int k = 0; k < 3; ++k) S.rot[k] = sg->axis[k];
+        }
+        double* R = Rs[i];
+        if (j >= 0) {
+            double Rq[9];
+            rot2(sg->axis, qv, Rq);
+            rotmul(sg->rot, Rq, R);
+        } else {
+            memcpy(R, sg->rot, sizeof(double) * 9);
+        }
+        const double* p = sg->trans;
+        twist_t vj, xv, xa, c;
+        for (int k = 0; k < 3; ++k) { vj.vel[k] = S.vel[k] * qdv; vj.rot[k] = S.rot[k] * qdv; }
+        if (i == 0) {
+            v = vj;
+            frame_inv_twist(R, p, &ag, &xa);
+        } else {
+            frame_inv_twist(R, p, &v, &xv);
+            frame_inv_twist(R, p, &a, &xa);
+            for (int k = 0; k < 3; ++k) { v.vel[k] = xv.vel[k] + vj.vel[k]; v.rot[k] = xv.rot[k] + vj.rot[k]; }
+        }
+        twist_cross(&v, &vj, &c);
+        for (int k = 0; k < 3; ++k) {
+            a.vel[k] = xa.vel[k] + S.vel[k] * qddv + c.vel[k];
+            a.rot[k] = xa.rot[k] + S.rot[k] * qddv + c.rot[k];
+        }
+        wrench_t Ia, Iv, vIv;
+        const double m = P->rb_m[i];
+        const double* h = P->rb_h + 3 * i;
+        const double* I = P->rb_I + 9 * i;
+        rbi_mul(m, h, I, &a, &Ia);
+        rbi_mul(m, h, I, &v, &Iv);
+        twist_cross_wrench(&v, &Iv, &vIv);
+        for (int k = 0; k < 3; ++k) { f[i].force[k] = Ia.force[k] + vIv.force[k]; f[i].torque[k] = Ia.torque[k] + vIv.torque[k]; }
+    }
+    for (int i = P->nchain - 1; i >= 0; --i) {
+        const so_segment* sg = &P->segs[P->chain[i]];
+        if (sg->q_index >= 0) {
+            /* dot(Twist, Wrench) = v . f + w . n with S = (0, axis) */
+            const double* n = f[i].torque;
+            const double* ff = f[i].force;
+            tau[sg->q_index] = (0.0 * ff[0] + 0.0 * ff[1] + 0.0 * ff[2]) + (sg->axis[0] * n[0] + sg->axis[1] * n[1] + sg->axis[2] * n[2]);
+        }
+        if (i != 0) {
+            wrench_t t;
+            frame_wrench(Rs[i], P->segs[P->chain[i]].trans, &f[i], &t);
+            for (int k = 0; k < 3; ++k) { f[i - 1].force[k] += t.force[k]; f[i - 1].torque[k] += t.torque[k]; }
+        }
+    }
+    return 0;
+}
+
+/* StompOptimizer::getTorques (stomp_optimizer.cpp:1033-1061) + the torque sum of execute
+ * (:1117-1142): q from the group trajectory row i, q-dot / q-ddot by the 7-tap rules of
+ * StompTrajectory::getJointVelocities / getJointAccelerations (stomp_trajectory.h:286-310) */
+static double torque_cost_at(const so_problem* P, const double* traj /* Nall x J */, int i)
+{
+    const int J = P->J;
+    double q[SO_MAX_J], qd[SO_MAX_J], qdd[SO_MAX_J], tau[SO_MAX_J];
+    const double invTime = 1.0 / P->disc, invTime2 = 1.0 / (P->disc * P->disc);
+    for (int j = 0; j < J; ++j) { q[j] = traj[(size_t)i * J + j]; qd[j] = 0.0; qdd[j] = 0.0; }
+    for (int k = -SO_DIFF_RULE_LENGTH / 2; k <= SO_DIFF_RULE_LENGTH / 2; ++k) {
+        const double cv = invTime * DIFF_RULES[0][k + SO_DIFF_RULE_LENGTH / 2];
+        const double ca = invTime2 * DIFF_RULES[1][k + SO_DIFF_RULE_LENGTH / 2];
+        for (int j = 0; j < J; ++j) {
+            qd[j] += cv * traj[(size_t)(i + k) * J + j];
+            qdd[j] += ca * traj[(size_t)(i + k) * J + j];
+        }
+    }
+    so_inverse_dynamics(P, q, qd, qdd, tau);
+    double s = 0.0;
+    for (int j = 0; j < J; ++j) s += fabs(tau[j]);
+    return s;
+}
+
 /* ---------------------------------------------------------------- distance field
  * distance_field::PropagationDistanceField::getDistanceGradient (3rd party; call site
  * stomp_collision_space.h:187-191): nearest cell = round((p - origin) * (1/res)) (VoxelGrid
@@ -312,6 +507,7 @@ void so_destroy(so_problem* P)
     free(P->tmp_params); free(P->tmp_noise); free(P->tmp_nproj); free(P->tmp_ctrl); free(P->tmp_prob);
     free(P->tmp_state);
     free(P->last_traj); free(P->best_traj);
+    free(P->chain); free(P->rb_m); free(P->rb_h); free(P->rb_I);
     free((void*)P->cfg.noise_stddev); free((void*)P->cfg.noise_decay);
     free((void*)P->cfg.start); free((void*)P->cfg.goal);
     free(P);
@@ -335,8 +531,12 @@ so_problem* so_create(const so_config* cfg)
         set_err("Number of reused rollouts must be strictly less than number of rollouts.");
         return NULL;
     }
-    if (cfg->torque_cost_weight > 1e-9) {
-        set_err("torque cost (stomp_optimizer.cpp:1120-1142) is not built in this round");
+    if (cfg->num_joints > SO_MAX_J) {
+        set_err("at most 32 joints");
+        return NULL;
+    }
+    if (cfg->num_orientation_constraints > 0) {
+        set_err("orientation constraints are not built yet");
         return NULL;
     }
     so_problem* P = (so_problem*)calloc(1, sizeof(so_problem));
@@ -374,6 +574,43 @@ so_problem* so_create(const so_config* cfg)
             so_destroy(P);
             return NULL;
         }
+
+    /* the inverse-dynamics chain (stomp_robot_model.cpp:185-189): segments below torque_root
+     * up to torque_tip; its joints must be the group's, in order */
+    P->torque = cfg->torque_cost_weight > 1e-9;
+    if (P->torque) {
+        const char* why = NULL;
+        int path[SO_MAX_CHAIN], n = 0;
+        if (!cfg->inertias) why = "torque term needs segment inertias";
+        else if (cfg->torque_root < 0 || cfg->torque_root >= P->nseg || cfg->torque_tip < 0 || cfg->torque_tip >= P->nseg)
+            why = "torque chain root/tip out of range";
+        else {
+            for (int sgi = cfg->torque_tip; sgi != cfg->torque_root; sgi = P->segs[sgi].parent) {
+                if (sgi < 0 || n == SO_MAX_CHAIN) { why = "torque tip is not below the torque root (or chain too long)"; break; }
+                path[n++] = sgi;
+            }
+        }
+        if (!why) {
+            int nj = 0;
+            for (int i = n - 1; i >= 0; --i)
+                if (P->segs[path[i]].q_index >= 0 && P->segs[path[i]].q_index != nj++) why = "torque chain joints must be the group joints in order";
+            if (!why && nj != J) why = "torque chain joints must be the group joints in order";
+        }
+        if (why) {
+            set_err(why);
+            so_destroy(P);
+            return NULL;
+        }
+        P->nchain = n;
+        P->chain = (int*)malloc(sizeof(int) * (size_t)n);
+        P->rb_m = dalloc((size_t)n);
+        P->rb_h = dalloc((size_t)n * 3);
+        P->rb_I = dalloc((size_t)n * 9);
+        for (int i = 0; i < n; ++i) {
+            P->chain[i] = path[n - 1 - i];
+            rb_inertia(&cfg->inertias[P->chain[i]], &P->rb_m[i], P->rb_h + 3 * i, P->rb_I + 9 * i);
+        }
+    }
 
     P->disc = cfg->discretization;
     /* group trajectory duration (N_all-1)*disc, truncated by getDuration() -> int
@@ -671,9 +908,10 @@ static void execute_one(const so_problem* P, exec_scratch* sc, const double* par
             cum += sc->pot[(size_t)i * S + j] * vmag;
             state += cum;
         }
-        /* stomp_optimizer.cpp:1148-1151; no constraints, torque weight 0 */
+        /* stomp_optimizer.cpp:1117-1151 */
+        const double tq = P->torque ? torque_cost_at(P, traj, i) : 0.0;
         double c = P->cfg.obstacle_cost_weight * state + P->cfg.constraint_cost_weight * 0.0 +
-                   P->cfg.torque_cost_weight * 0.0;
+                   P->cfg.torque_cost_weight * tq;
         costs[i - SO_PAD] = c;
     }
     for (int t = 0; t < N; ++t) sum = (t == 0) ? costs[0] : sum + costs[t];   /* costs.sum() :1155 */

@@ -67,6 +67,26 @@ typedef struct {
     const float* data;
 } so_sdf;
 
+/* KDL::RigidBodyInertia(m, cog, Ic) of a segment, in the segment frame; Ic is about the
+ * centre of mass, (Ixx, Iyy, Izz, Ixy, Ixz, Iyz) */
+typedef struct {
+    double mass;
+    double com[3];
+    double inertia[6];
+} so_inertia;
+
+/* motion_planning_msgs::OrientationConstraint as stored by OrientationConstraintEvaluator
+ * (constraint_evaluator.cpp:50-73) */
+typedef struct {
+    int segment;                /* frame_number_ (segmentNameToIndex(link_name)) */
+    double orientation[4];      /* nominal quaternion x, y, z, w */
+    int body_fixed;             /* type != HEADER_FRAME */
+    double absolute_roll_tolerance;
+    double absolute_pitch_tolerance;
+    double absolute_yaw_tolerance;
+    double weight;
+} so_orientation_constraint;
+
 typedef struct {
     int num_joints;             /* J */
     int num_time_steps;         /* N (free waypoints) */
@@ -84,7 +104,7 @@ typedef struct {
     double smoothness_cost_weight;
     double obstacle_cost_weight;
     double constraint_cost_weight;
-    double torque_cost_weight;  /* must be <= 1e-9: torque term not built yet */
+    double torque_cost_weight;  /* > 1e-9: torque term (stomp_optimizer.cpp:1117-1142) */
     const double* noise_stddev; /* J */
     const double* noise_decay;  /* J */
     int use_cumulative_costs;
@@ -96,6 +116,14 @@ typedef struct {
     int sum_block;              /* canonical blocked sum over rollouts (64); 0 -> 64 */
     int dense;                  /* 1: dense N x N products exactly as the reference (CPU baseline) */
     int threads;                /* OpenMP threads over rollouts (1 = reference) */
+    /* torque term: KDL::ChainIdSolver_RNE over getChain(root, tip) (stomp_robot_model.cpp:185-189) */
+    const so_inertia* inertias; /* num_segments (NULL: torque term off) */
+    int torque_root;            /* chain base segment (exclusive) */
+    int torque_tip;             /* chain tip segment (inclusive) */
+    double gravity[3];          /* in the frame of torque_root */
+    /* path constraints (stomp_optimizer.cpp:195-201, 1107-1115) */
+    int num_orientation_constraints;
+    const so_orientation_constraint* orientation_constraints;
 } so_config;
 
 typedef struct so_problem so_problem;
@@ -104,6 +132,9 @@ typedef struct {
     double cost;                /* last_trajectory_cost_ of the noiseless rollout */
     int collision_free;         /* last_trajectory_collision_free_ */
 } so_iter_out;
+
+/* KDL::ChainIdSolver_RNE::CartToJnt on the torque chain, group joint vectors of length J */
+int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, const double* qdd, double* tau);
 
 typedef struct {
     int iterations;             /* iterations run */

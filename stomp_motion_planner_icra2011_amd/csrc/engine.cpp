@@ -31,8 +31,8 @@ namespace {
 
 thread_local std::string g_last_error;
 
-enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_COUNT };
-const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse"};
+enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_TERMS, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse", "state_terms"};
 
 }  // namespace
 
@@ -51,6 +51,9 @@ struct stomp_engine {
     std::vector<double> sig_std, sig_dec, start, goal;
     SetupOutput su;
     DevModel model{};
+    TermsModel terms{};
+    bool terms_on = false;      // torque term / path constraints: k_terms after every k_rollout
+    double* d_terms_traj = nullptr;   // [K_loc][J][N] joint-limited trajectories for k_terms
     std::vector<FkOp> ops;
     std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
     int nslots = 0;
@@ -247,6 +250,28 @@ int plan_fk(stomp_engine* e, const stomp_engine_desc* d, std::vector<FkOp>& ops)
     return 0;
 }
 
+// the torque term's chain (stomp_robot_model.cpp:185-189): segments below torque_root up to
+// torque_tip, root side first; its joints must be the group's joints in order.  Returns an
+// error message, or nullptr.
+const char* torque_chain(const stomp_engine_desc* d, std::vector<int>& path)
+{
+    path.clear();
+    if (!d->inertias) return "torque term needs segment inertias";
+    if (d->torque_root < 0 || d->torque_root >= d->num_segments || d->torque_tip < 0 ||
+        d->torque_tip >= d->num_segments)
+        return "torque chain root/tip out of range";
+    for (int sgi = d->torque_tip; sgi != d->torque_root; sgi = d->segments[sgi].parent) {
+        if (sgi < 0 || (int)path.size() == kMaxChain) return "torque tip is not below the torque root (or chain too long)";
+        path.push_back(sgi);
+    }
+    std::reverse(path.begin(), path.end());
+    int nj = 0;
+    for (int sgi : path)
+        if (d->segments[sgi].q_index >= 0 && d->segments[sgi].q_index != nj++) return "torque chain joints must be the group joints in order";
+    if (nj != d->num_joints) return "torque chain joints must be the group joints in order";
+    return nullptr;
+}
+
 void release(stomp_engine* e)
 {
     if (!e) return;
@@ -262,15 +287,32 @@ void release(stomp_engine* e)
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
 }
 
+// the state-cost terms after the collision cost (k_terms), on the rollouts a k_rollout
+// launch with these arguments evaluated; its trajectories must have been written
+void launch_terms_for(stomp_engine* e, const CostArgs& ca)
+{
+    if (!e->terms_on) return;
+    Timed tm(e, T_TERMS);
+    TermsArgs ta{};
+    ta.traj = ca.traj_out; ta.state = ca.state_out; ta.total = ca.total_out; ta.num_noisy = ca.num_noisy;
+    if (ca.x_params) {
+        ta.x_traj = ca.x_traj; ta.x_state = ca.x_state; ta.x_total = ca.x_total;
+    }
+    launch_terms(e->terms, ta, e->stream);
+}
+
 // noiseless rollout of the current theta (policy_improvement_loop.cpp:180-182), alone
 void launch_noiseless(stomp_engine* e, int member)
 {
-    Timed tm(e, T_NOISELESS);
     CostArgs ca{};
     ca.num_noisy = 0;
     ca.x_params = e->d_theta; ca.x_member = member;
     ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
-    launch_cost(e->model, ca, e->stream);
+    {
+        Timed tm(e, T_NOISELESS);
+        launch_cost(e->model, ca, e->stream);
+    }
+    launch_terms_for(e, ca);
 }
 
 int flush_noiseless(stomp_engine* e)
@@ -342,13 +384,17 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         ca.nz = na;
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
+        if (e->terms_on) ca.traj_out = e->d_terms_traj;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
             ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
             e->pending_member = -1;
         }
-        Timed tm(e, T_COST);
-        launch_cost(e->model, ca, e->stream);
+        {
+            Timed tm(e, T_COST);
+            launch_cost(e->model, ca, e->stream);
+        }
+        launch_terms_for(e, ca);
     }
     WeightArgs wa{};
     wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
@@ -439,8 +485,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (d->num_rollouts <= 0) return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be positive");
     if (d->num_reused_rollouts < 0 || d->num_reused_rollouts >= d->num_rollouts)
         return fail(nullptr, STOMP_E_INVALID, "Number of reused rollouts must be strictly less than number of rollouts.");
-    if (d->torque_cost_weight > 1e-9)
-        return fail(nullptr, STOMP_E_UNSUPPORTED, "torque cost (stomp_optimizer.cpp:1120-1142) is not built yet");
+    if (d->num_orientation_constraints > 0)
+        return fail(nullptr, STOMP_E_UNSUPPORTED, "orientation constraints are not built yet");
     if (d->num_segments <= 0 || !d->segments || (d->num_spheres > 0 && !d->spheres) || !d->joints || !d->noise_stddev ||
         !d->noise_decay || !d->start || !d->goal || !d->grid.data)
         return fail(nullptr, STOMP_E_INVALID, "missing table pointer");
@@ -454,6 +500,10 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     for (int j = 0; j < d->num_spheres; ++j)
         if (d->spheres[j].segment < 0 || d->spheres[j].segment >= d->num_segments)
             return fail(nullptr, STOMP_E_INVALID, "sphere %d: bad segment", j);
+    if (d->torque_cost_weight > 1e-9) {
+        std::vector<int> path;
+        if (const char* why = torque_chain(d, path)) return fail(nullptr, STOMP_E_UNSUPPORTED, "%s", why);
+    }
     const int world = d->world_size > 0 ? d->world_size : 1;
     if (world > 1) {
         if (d->num_reused_rollouts > 0)
@@ -607,6 +657,50 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (hipHostMalloc((void**)&e->h_total, sizeof(double)) != hipSuccess ||
         hipHostMalloc((void**)&e->h_cf, 16) != hipSuccess)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
+
+    // the torque term's chain (stomp_robot_model.cpp:185-189): segments below torque_root up to
+    // torque_tip, whose joints must be the group's joints in order
+    if (d->torque_cost_weight > 1e-9) {
+        std::vector<int> path;
+        torque_chain(d, path);
+        std::vector<ChainSeg> cs(path.size());
+        for (size_t i = 0; i < path.size(); ++i) {
+            cs[i].seg = segs[path[i]];
+            // KDL::RigidBodyInertia(m, c, Ic): h = m c, I = Ic - m (c c^T - (c.c) 1)
+            const stomp_inertia& in = d->inertias[path[i]];
+            const double* c = in.com;
+            const double* v = in.inertia;
+            const double Ic[9] = {v[0], v[3], v[4], v[3], v[1], v[5], v[4], v[5], v[2]};
+            const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+            cs[i].m = in.mass;
+            for (int a = 0; a < 3; ++a) {
+                cs[i].h[a] = in.mass * c[a];
+                for (int b = 0; b < 3; ++b) cs[i].I[3 * a + b] = Ic[3 * a + b] - in.mass * (c[a] * c[b] - (a == b ? cc : 0.0));
+            }
+        }
+        ChainSeg* d_chain;
+        CREATE_TRY(upload(e, &d_chain, cs.data(), cs.size()));
+        TermsModel& t = e->terms;
+        t.torque = 1;
+        t.nchain = (int)cs.size();
+        t.chain = d_chain;
+        for (int k = 0; k < 3; ++k) t.g[k] = d->gravity[k];
+        e->terms_on = true;
+    }
+    if (e->terms_on) {
+        TermsModel& t = e->terms;
+        t.J = J; t.N = N;
+        const double invTime = 1.0 / e->disc, invTime2 = 1.0 / (e->disc * e->disc);   // stomp_trajectory.h:289, 301
+        for (int k = 0; k < 7; ++k) {
+            t.cv[k] = invTime * kDiffRules[0][k];
+            t.ca[k] = invTime2 * kDiffRules[1][k];
+        }
+        t.start = e->d_start; t.goal = e->d_goal;
+        t.w_con = e->w_con; t.w_tq = e->w_tq;
+        if (terms_lds_bytes(t) > 160 * 1024)
+            CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "state-terms kernel needs %zu B of LDS", terms_lds_bytes(t)));
+        CREATE_TRY(dev_alloc(e, &e->d_terms_traj, KJN));
+    }
 
     DevModel& m = e->model;
     m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size(); m.nseg = e->nseg;
@@ -775,8 +869,10 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
     HIP_TRY(e, hipMemcpyAsync(e->d_eval_params, params, sizeof(double) * num * JN, hipMemcpyHostToDevice, e->stream));
     CostArgs ca{};
     ca.params = e->d_eval_params; ca.stride = (long long)JN; ca.num_noisy = num; ca.member = iteration_member;
-    ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf; ca.traj_out = traj_out ? e->d_eval_traj : nullptr;
+    ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf;
+    ca.traj_out = (traj_out || e->terms_on) ? e->d_eval_traj : nullptr;
     launch_cost(e->model, ca, e->stream);
+    launch_terms_for(e, ca);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipMemcpyAsync(costs, e->d_eval_costs, sizeof(double) * num * e->N, hipMemcpyDeviceToHost, e->stream));
     if (collision_free)

@@ -176,6 +176,41 @@ struct WeightArgs {
     double* u_part;             // [nb_loc][J][N]   USUM writes
 };
 
+// The state-cost terms that StompOptimizer::execute adds after the collision cost
+// (stomp_optimizer.cpp:1107-1151): the torque term (KDL::ChainIdSolver_RNE on the
+// inverse-dynamics chain, :1117-1142).  k_terms runs after k_rollout on the same rollouts,
+// reading the joint-limited trajectories k_rollout wrote, and finishes
+// costs(t) = (w_obs state + w_con con) + w_tq tq in the reference's order.
+constexpr int kMaxChain = 32;
+
+struct ChainSeg {
+    DevSegment seg;             // pose(q) of the chain segment (parent = previous chain segment)
+    double m, h[3], I[9];       // KDL::RigidBodyInertia about the segment origin (h = m c)
+};
+
+struct TermsModel {
+    int J, N, nchain, torque;
+    const ChainSeg* chain;      // [nchain], root side first
+    double g[3];                // gravity in the chain root frame
+    double cv[7], ca[7];        // invTime * DIFF_RULES[0][k], invTime^2 * DIFF_RULES[1][k]
+    const double* start;        // [J]
+    const double* goal;         // [J]
+    double w_con, w_tq;
+};
+
+struct TermsArgs {
+    const double* traj;         // [num_noisy][J][N] joint-limited trajectories
+    double* state;              // [num_noisy][N] in: w_obs * collision cost; out: the full costs
+    double* total;              // [num_noisy] or null
+    int num_noisy;
+    const double* x_traj;       // the extra (noiseless) rollout, or null
+    double* x_state;
+    double* x_total;
+};
+
+size_t terms_lds_bytes(const TermsModel& m);
+void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
+
 void launch_noise(const NoiseArgs& a, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);

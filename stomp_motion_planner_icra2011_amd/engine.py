@@ -14,7 +14,7 @@ import numpy as np
 from . import _build
 
 _LIB_PATH = _build.LIB
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class stomp_segment(C.Structure):
@@ -35,6 +35,16 @@ class stomp_grid(C.Structure):
                 ("resolution", C.c_double), ("data", C.c_void_p), ("data_on_device", C.c_int32)]
 
 
+class stomp_inertia(C.Structure):
+    _fields_ = [("mass", C.c_double), ("com", C.c_double * 3), ("inertia", C.c_double * 6)]
+
+
+class stomp_orientation_constraint(C.Structure):
+    _fields_ = [("segment", C.c_int32), ("orientation", C.c_double * 4), ("body_fixed", C.c_int32),
+                ("absolute_roll_tolerance", C.c_double), ("absolute_pitch_tolerance", C.c_double),
+                ("absolute_yaw_tolerance", C.c_double), ("weight", C.c_double)]
+
+
 class stomp_engine_desc(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("num_joints", C.c_int32), ("num_time_steps", C.c_int32),
                 ("num_rollouts", C.c_int32), ("num_reused_rollouts", C.c_int32), ("num_segments", C.c_int32),
@@ -47,7 +57,10 @@ class stomp_engine_desc(C.Structure):
                 ("use_cumulative_costs", C.c_int32), ("start", C.POINTER(C.c_double)),
                 ("goal", C.POINTER(C.c_double)), ("seed", C.c_uint64), ("max_iterations", C.c_int32),
                 ("max_iterations_after_collision_free", C.c_int32), ("device", C.c_int32), ("stream", C.c_void_p),
-                ("rank", C.c_int32), ("world_size", C.c_int32), ("comm_id", C.c_void_p)]
+                ("rank", C.c_int32), ("world_size", C.c_int32), ("comm_id", C.c_void_p),
+                ("inertias", C.POINTER(stomp_inertia)), ("torque_root", C.c_int32), ("torque_tip", C.c_int32),
+                ("gravity", C.c_double * 3), ("num_orientation_constraints", C.c_int32),
+                ("orientation_constraints", C.POINTER(stomp_orientation_constraint))]
 
 
 class stomp_iter_out(C.Structure):
@@ -204,6 +217,22 @@ class Engine:
         d.world_size = world_size
         self._comm = C.create_string_buffer(comm_id, 128) if comm_id else None
         d.comm_id = C.cast(self._comm, C.c_void_p) if comm_id else None
+        nseg = len(p.robot.segments)
+        self._inertia = (stomp_inertia * nseg)(*[
+            stomp_inertia(s.inertia.mass, (C.c_double * 3)(*s.inertia.com), (C.c_double * 6)(*s.inertia.inertia))
+            if s.inertia else stomp_inertia() for s in p.robot.segments])
+        d.inertias = self._inertia
+        d.torque_root = p.robot.index(p.torque_root)
+        d.torque_tip = p.robot.index(p.torque_tip)
+        d.gravity = (C.c_double * 3)(*p.gravity)
+        oc = p.orientation_constraints
+        self._oc = (stomp_orientation_constraint * max(len(oc), 1))(*[
+            stomp_orientation_constraint(p.robot.index(c.link_name), (C.c_double * 4)(*c.orientation),
+                                         0 if c.header_frame else 1, c.absolute_roll_tolerance,
+                                         c.absolute_pitch_tolerance, c.absolute_yaw_tolerance, c.weight)
+            for c in oc])
+        d.num_orientation_constraints = len(oc)
+        d.orientation_constraints = self._oc
         self._desc = d
         h = C.c_void_p()
         _check(l.stomp_engine_create(C.byref(d), C.byref(h)))

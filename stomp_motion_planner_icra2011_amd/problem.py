@@ -36,6 +36,7 @@ class Segment:
     trans: Sequence[float]
     axis: Sequence[float] = (0.0, 0.0, 1.0)
     rot: Sequence[float] = (1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0)
+    inertia: Optional["Inertia"] = None   # None: massless
 
 
 @dataclasses.dataclass
@@ -54,6 +55,28 @@ class Sphere:
     clearance: float
     pos: Sequence[float]
     link: str = ""
+
+
+@dataclasses.dataclass
+class Inertia:
+    """KDL::RigidBodyInertia(m, cog, Ic) of a segment, in the segment frame; Ic about the
+    centre of mass as (Ixx, Iyy, Izz, Ixy, Ixz, Iyz)."""
+    mass: float
+    com: Sequence[float] = (0.0, 0.0, 0.0)
+    inertia: Sequence[float] = (0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+
+
+@dataclasses.dataclass
+class OrientationConstraint:
+    """motion_planning_msgs::OrientationConstraint as consumed by
+    OrientationConstraintEvaluator (constraint_evaluator.cpp:50-73)."""
+    link_name: str
+    orientation: Sequence[float]  # quaternion (x, y, z, w)
+    header_frame: bool = False    # type == HEADER_FRAME (else body-fixed)
+    absolute_roll_tolerance: float = math.pi
+    absolute_pitch_tolerance: float = math.pi
+    absolute_yaw_tolerance: float = math.pi
+    weight: float = 1.0
 
 
 @dataclasses.dataclass
@@ -85,6 +108,34 @@ _LINK_RADII = [
 COLLISION_CLEARANCE = 0.07  # pr2_both_arms_stomp_config.yaml:1
 
 
+# Synthetic PR2-like link inertias (mass kg, centre of mass m, inertia about it kg m^2).  The
+# PR2 URDF is not in the container; the masses follow the published PR2 arm figures and the
+# centres / inertias are rod-like estimates, so the torque term is exercised on a realistic
+# scale.  Links not listed (finger links, tool frame) are massless.
+_LINK_INERTIA = {
+    "shoulder_pan_link": Inertia(25.8, (-0.032, 0.0, -0.27), (0.866, 0.874, 0.273, -0.006, 0.121, -0.059)),
+    "shoulder_lift_link": Inertia(2.75, (0.0, 0.0, 0.0), (0.021, 0.021, 0.020, 0.0, 0.0, 0.0)),
+    "upper_arm_roll_link": Inertia(0.1, (0.0, 0.0, 0.0), (0.01, 0.01, 0.01, 0.0, 0.0, 0.0)),
+    "upper_arm_link": Inertia(6.01, (0.216, 0.0, -0.0003), (0.015, 0.0747, 0.0761, -0.0012, 0.0087, -0.0001)),
+    "elbow_flex_link": Inertia(1.9, (0.01, 0.0, -0.012), (0.0035, 0.0044, 0.0031, 0.0, 0.0001, 0.0)),
+    "forearm_roll_link": Inertia(0.1, (0.0, 0.0, 0.0), (0.01, 0.01, 0.01, 0.0, 0.0, 0.0)),
+    "forearm_link": Inertia(2.57, (0.181, 0.0, 0.0), (0.0037, 0.0150, 0.0166, 0.0001, 0.0, 0.0)),
+    "wrist_flex_link": Inertia(0.61, (-0.0016, 0.0, 0.0), (0.0007, 0.0007, 0.0006, 0.0, 0.0, 0.0)),
+    "wrist_roll_link": Inertia(0.1, (0.0, 0.0, 0.0), (0.01, 0.01, 0.01, 0.0, 0.0, 0.0)),
+    "gripper_palm_link": Inertia(0.58, (0.06, 0.0, 0.0), (0.0004, 0.0011, 0.0010, 0.0, 0.0, 0.0)),
+}
+
+
+def _set_inertia(segs, name: str, sign: float, inertia: Inertia):
+    for s in segs:
+        if s.name == name:
+            c = (inertia.com[0], sign * inertia.com[1], inertia.com[2])
+            i = inertia.inertia
+            s.inertia = Inertia(inertia.mass, c, (i[0], i[1], i[2], sign * i[3], i[4], sign * i[5]))
+            return
+    raise KeyError(name)
+
+
 def _arm(prefix: str, sign: float, parent: int, q0: int, segs: List[Segment], joints: List[Joint]):
     """PR2 arm chain below the torso (PR2 URDF offsets)."""
     def add(name, q, trans, axis=(0.0, 0.0, 1.0), par=None):
@@ -106,6 +157,8 @@ def _arm(prefix: str, sign: float, parent: int, q0: int, segs: List[Segment], jo
     rf = add("gripper_r_finger_link", -1, (0.07691, -0.01, 0.0), par=palm)
     add("gripper_r_finger_tip_link", -1, (0.09137, -0.00495, 0.0), par=rf)
     add("gripper_tool_frame", -1, (0.18, 0.0, 0.0), par=palm)
+    for name, inertia in _LINK_INERTIA.items():
+        _set_inertia(segs, prefix + name, sign, inertia)
     if sign > 0:  # right arm limits (PR2 URDF)
         lim = [(-2.2853981634, 0.714601836603), (-0.5236, 1.3963), (-3.9, 0.8), (-2.3213, 0.0),
                None, (-2.18, 0.0), None]
@@ -319,6 +372,23 @@ class Problem:
     goal: np.ndarray
     seed: int = 0x53544F4D50000000
     sdf: Optional[np.ndarray] = None
+    # inverse-dynamics chain of the torque term: KDL getChain("torso_lift_link",
+    # "r_gripper_tool_frame") with gravity (0, 0, -9.8) (stomp_robot_model.cpp:185-189)
+    torque_root: str = "torso_lift_link"
+    torque_tip: str = "r_gripper_tool_frame"
+    gravity: Sequence[float] = (0.0, 0.0, -9.8)
+    orientation_constraints: List[OrientationConstraint] = dataclasses.field(default_factory=list)
+
+    def torque_chain(self) -> List[int]:
+        """Segment indices of the chain root (exclusive) -> tip (inclusive), root side first."""
+        r, s = self.robot.index(self.torque_root), self.robot.index(self.torque_tip)
+        out = []
+        while s != r:
+            if s < 0:
+                raise ValueError("torque tip is not below the torque root")
+            out.append(s)
+            s = self.robot.segments[s].parent
+        return out[::-1]
 
     @property
     def J(self) -> int:

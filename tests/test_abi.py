@@ -44,6 +44,7 @@ def test_struct_layouts_match_c(tmp_path):
     structs = {"stomp_segment": eng.stomp_segment, "stomp_sphere": eng.stomp_sphere,
                "stomp_joint": eng.stomp_joint, "stomp_grid": eng.stomp_grid,
                "stomp_engine_desc": eng.stomp_engine_desc, "stomp_iter_out": eng.stomp_iter_out,
+               "stomp_inertia": eng.stomp_inertia, "stomp_orientation_constraint": eng.stomp_orientation_constraint,
                "stomp_stats": eng.stomp_stats}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "stomp_engine.h"', "int main(void){"]
     for name, cls in structs.items():
@@ -72,10 +73,15 @@ def test_header_compiles_as_c_and_cpp(tmp_path):
 
 @pytest.mark.parametrize("kw,code,msg", [
     (dict(num_rollouts=10, num_reused_rollouts=10), -1, "strictly less"),
-    (dict(num_rollouts=10, num_reused_rollouts=0, torque_cost_weight=0.001), -3, "torque"),
+    (dict(dof=14, num_rollouts=10, num_reused_rollouts=0, torque_cost_weight=0.001), -3, "group joints"),
+    (dict(num_rollouts=10, num_reused_rollouts=0, torque_cost_weight=0.001, torque_tip="torso_lift_link"), -3,
+     "group joints"),
 ])
 def test_create_validates_before_touching_the_device(kw, code, msg):
+    tip = kw.pop("torque_tip", None)
     p = pb.make_problem(grid_n=16, **kw)
+    if tip:
+        p.torque_tip = tip
     with pytest.raises(RuntimeError) as ei:
         eng.Engine(p)
     assert f"error {code}" in str(ei.value) and msg in str(ei.value)

@@ -1,0 +1,61 @@
+"""GPU parity of the state-cost terms after the collision cost (SURVEY.md §8a rows a12b and
+a13, stomp_optimizer.cpp:1107-1151): k_terms through the C ABI against the CPU oracle, bit for
+bit, in batched Task::execute, in iterations (with rollout reuse) and in the optimize loop."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from stomp_motion_planner_icra2011_amd import engine as eng
+from stomp_motion_planner_icra2011_amd import problem as pb
+
+pytestmark = pytest.mark.gpu
+
+
+def make(K=10, Kr=0, waypoints=100, **kw):
+    kw.setdefault("torque_cost_weight", 0.001)
+    return pb.make_problem(grid_n=64, waypoints=waypoints, num_rollouts=K, num_reused_rollouts=Kr, **kw)
+
+
+def _compare_iteration(o, e, it):
+    oc, ec = o.iterate(it), e.iterate(it)
+    assert ec == oc, (it, ec, oc)
+    for f in ("params", "noise", "control_costs", "state_costs", "probabilities"):
+        np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f"iteration {it} field {f}")
+    np.testing.assert_array_equal(e.theta(), o.theta())
+    np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory())
+
+
+@pytest.mark.parametrize("waypoints", [100, 40, 200])
+def test_torque_execute_bitwise(waypoints):
+    p = make(waypoints=waypoints)
+    o, e = po.Oracle(p), eng.Engine(p)
+    rng = np.random.default_rng(7)
+    th = o.theta()
+    params = th[None] + rng.standard_normal((5, p.J, p.N)).cumsum(axis=2) * 0.05
+    params[0] = th
+    params[4] += 3.0   # joint limits active
+    costs, cf, traj = e.execute(params, iteration_member=1)
+    for r in range(params.shape[0]):
+        oc, ocf, otr = o.execute(params[r], iteration_member=1)
+        np.testing.assert_array_equal(traj[r], otr)
+        np.testing.assert_array_equal(costs[r], oc)
+        assert bool(cf[r]) == ocf
+
+
+@pytest.mark.parametrize("K,Kr", [(10, 5), (130, 0)])
+def test_torque_iterations_bitwise(K, Kr):
+    p = make(K=K, Kr=Kr)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 6):
+        _compare_iteration(o, e, it)
+
+
+def test_torque_optimize_bitwise():
+    p = make(K=20, Kr=10, max_iterations=40, max_iterations_after_collision_free=40)
+    o, e = po.Oracle(p), eng.Engine(p)
+    ost, ocosts = o.optimize()
+    est, ecosts = e.optimize()
+    assert (est.iterations, est.success_iteration, est.last_improvement_iteration) == \
+        (ost.iterations, ost.success_iteration, ost.last_improvement_iteration)
+    np.testing.assert_array_equal(ecosts, ocosts)
+    np.testing.assert_array_equal(e.best_trajectory(), o.best_trajectory())
