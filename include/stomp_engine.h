@@ -159,6 +159,7 @@ typedef struct stomp_engine stomp_engine;
 typedef struct stomp_iter_out {
     double cost;                /* last_trajectory_cost_ of the noiseless rollout */
     int32_t collision_free;     /* last_trajectory_collision_free_ */
+    int32_t constraints_satisfied; /* last_trajectory_constraints_satisfied_ */
 } stomp_iter_out;
 
 /* STOMPStatistics (msg/STOMPStatistics.msg) without the ROS header / torques */
@@ -185,9 +186,11 @@ int stomp_engine_synchronize(stomp_engine* e);
 
 /* Batched Task::execute: params E x J x N, costs E x N, collision_free E,
  * traj_out E x J x N (joint-limit-corrected free block, may be NULL).
- * iteration_member is StompOptimizer::iteration_ (0: padding points count for the flag). */
+ * iteration_member is StompOptimizer::iteration_ (0: padding points count for the flag).
+ * constraints_satisfied E (last_trajectory_constraints_satisfied_, may be NULL). */
 int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double* costs,
-                      uint8_t* collision_free, double* traj_out, int32_t iteration_member);
+                      uint8_t* collision_free, double* traj_out, int32_t iteration_member,
+                      uint8_t* constraints_satisfied);
 
 int stomp_engine_optimize(stomp_engine* e, stomp_stats* stats, double* costs_per_iteration);
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj);

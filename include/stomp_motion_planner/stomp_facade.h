@@ -71,6 +71,18 @@ struct StompRobotModel {
     std::vector<stomp_segment> segments;
     std::vector<stomp_joint> joints;          // planning-group joints, J
     std::vector<stomp_sphere> collision_points;
+    // inverse dynamics of the torque term (stomp_robot_model.cpp:185-189): segment inertias
+    // and the chain torque_root (exclusive) -> torque_tip (inclusive); needed only when
+    // torque_cost_weight > 1e-9
+    std::vector<stomp_inertia> inertias;      // per segment
+    int torque_root = -1, torque_tip = -1;
+    double gravity[3] = {0.0, 0.0, -9.8};
+};
+
+// motion_planning_msgs::Constraints as StompOptimizer consumes it (stomp_optimizer.cpp:195-201):
+// orientation path constraints only
+struct Constraints {
+    std::vector<stomp_orientation_constraint> orientation_constraints;
 };
 
 // StompCollisionSpace's distance field (stomp_collision_space.h:187-191).
@@ -144,7 +156,8 @@ class StompOptimizer : public Task {
 public:
     // stomp_optimizer.cpp:50-70 (publishers and constraints not taken, see the file header)
     StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model, const StompParameters* parameters,
-                   StompCollisionSpace* collision_space, int device = 0, void* stream = nullptr);
+                   StompCollisionSpace* collision_space, const Constraints& constraints = Constraints(),
+                   int device = 0, void* stream = nullptr);
     ~StompOptimizer() override;
     StompOptimizer(const StompOptimizer&) = delete;
     StompOptimizer& operator=(const StompOptimizer&) = delete;
@@ -174,6 +187,7 @@ public:
     // last_trajectory_cost_ / last_trajectory_collision_free_ after runSingleIteration
     double lastTrajectoryCost() const { return last_cost_; }
     bool lastTrajectoryCollisionFree() const { return last_cf_; }
+    bool lastTrajectoryConstraintsSatisfied() const { return last_cs_; }
 
 private:
     friend class PolicyImprovementLoop;
@@ -186,6 +200,7 @@ private:
     int J_ = 0, N_ = 0;
     double last_cost_ = 0.0;
     bool last_cf_ = false;
+    bool last_cs_ = true;
     STOMPStatistics stats_;
     std::string error_;
 };

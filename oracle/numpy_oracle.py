@@ -227,3 +227,21 @@ def inverse_dynamics(problem, q, qd, qdd):
         if qi >= 0:
             tau[qi] = z @ n
     return tau
+
+
+def orientation_constraint_cost(c, R):
+    """Independent restatement of OrientationConstraintEvaluator::getCost
+    (constraint_evaluator.cpp:80-114) with scipy's rotation algebra: the orientation error
+    against the nominal orientation (header frame: R N^-1, body fixed: N^-1 R) as the
+    yaw-pitch-roll angles of R = Rz(yaw) Ry(pitch) Rx(roll), pitch in [-pi/2, pi/2]
+    (bullet getEulerYPR solution 1).  Returns (cost, satisfied)."""
+    from scipy.spatial.transform import Rotation
+    N = Rotation.from_quat(np.asarray(c.orientation, np.float64)).as_matrix()
+    E = R @ N.T if c.header_frame else N.T @ R
+    yaw, pitch, roll = np.abs(Rotation.from_matrix(E).as_euler("ZYX"))
+    w = [0.0 if tol >= math.pi else 1.0 for tol in
+         (c.absolute_roll_tolerance, c.absolute_pitch_tolerance, c.absolute_yaw_tolerance)]
+    cost = c.weight * (w[0] * roll + w[1] * pitch + w[2] * yaw)
+    ok = not (roll > c.absolute_roll_tolerance or pitch > c.absolute_pitch_tolerance or
+              yaw > c.absolute_yaw_tolerance)
+    return cost, ok

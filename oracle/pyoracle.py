@@ -62,7 +62,7 @@ class so_config(C.Structure):
 
 
 class so_iter_out(C.Structure):
-    _fields_ = [("cost", C.c_double), ("collision_free", C.c_int)]
+    _fields_ = [("cost", C.c_double), ("collision_free", C.c_int), ("constraints_satisfied", C.c_int)]
 
 
 class so_stats(C.Structure):
@@ -90,7 +90,7 @@ def lib():
         l.so_get_theta.argtypes = [P, dp]
         l.so_set_theta.argtypes = [P, dp]
         l.so_get_pad_positions.argtypes = [P, dp]
-        l.so_execute.argtypes = [P, dp, dp, C.POINTER(C.c_int), dp, C.c_int]
+        l.so_execute.argtypes = [P, dp, dp, C.POINTER(C.c_int), dp, C.c_int, C.POINTER(C.c_int)]
         l.so_iterate.argtypes = [P, C.c_int, C.POINTER(so_iter_out)]
         l.so_optimize.argtypes = [P, C.POINTER(so_stats), dp]
         l.so_get_best_trajectory.argtypes = [P, dp]
@@ -108,6 +108,10 @@ def lib():
         l.so_sdf_distance.argtypes = [P, C.c_double, C.c_double, C.c_double]
         l.so_potential.argtypes = [P, C.c_int, dp, dp]
         l.so_inverse_dynamics.argtypes = [P, dp, dp, dp, dp]
+        l.so_atan2.restype = C.c_double
+        l.so_atan2.argtypes = [C.c_double, C.c_double]
+        l.so_asin.restype = C.c_double
+        l.so_asin.argtypes = [C.c_double]
         _lib = l
     return _lib
 
@@ -223,13 +227,15 @@ class Oracle:
         prm = np.ascontiguousarray(params, np.float64)
         costs = np.zeros(self.N)
         traj = np.zeros((self.J, self.N))
-        cf = C.c_int()
-        lib().so_execute(self.h, _dp(prm), _dp(costs), C.byref(cf), _dp(traj), iteration_member)
+        cf, cs = C.c_int(), C.c_int()
+        lib().so_execute(self.h, _dp(prm), _dp(costs), C.byref(cf), _dp(traj), iteration_member, C.byref(cs))
+        self.last_constraints_satisfied = bool(cs.value)
         return costs, bool(cf.value), traj
 
     def iterate(self, iteration_number: int):
         o = so_iter_out()
         lib().so_iterate(self.h, iteration_number, C.byref(o))
+        self.last_constraints_satisfied = bool(o.constraints_satisfied)
         return o.cost, bool(o.collision_free)
 
     def optimize(self):
@@ -298,6 +304,14 @@ def dexp(x: float) -> float:
 
 def dlog(x: float) -> float:
     return lib().so_log(x)
+
+
+def datan2(y: float, x: float) -> float:
+    return lib().so_atan2(y, x)
+
+
+def dasin(x: float) -> float:
+    return lib().so_asin(x)
 
 
 def dsincos(x: float):

@@ -68,6 +68,10 @@ struct so_problem {
     double* rb_m;          /* nchain */
     double* rb_h;          /* nchain x 3: m c */
     double* rb_I;          /* nchain x 9: rotational inertia about the segment origin */
+    /* path constraints */
+    int noc;
+    struct oc_eval* oc;
+    int last_cs;           /* last_trajectory_constraints_satisfied_ */
 };
 
 /* ---------------------------------------------------------------- linear algebra */
@@ -182,6 +186,8 @@ void so_normals(uint64_t seed, int iteration, int joint, int rollout, int n, dou
 double so_exp(double x) { return dm_exp(x); }
 double so_log(double x) { return dm_log(x); }
 void so_sincos(double x, double* s, double* c) { dm_sincos(x, s, c); }
+double so_atan2(double y, double x) { return dm_atan2(y, x); }
+double so_asin(double x) { return dm_asin(x); }
 
 /* ---------------------------------------------------------------- KDL frames
  * KDL::Rotation::Rot2 / Rotation*Rotation / Rotation*Vector / Frame*Frame as in
@@ -442,6 +448,154 @@ static double torque_cost_at(const so_problem* P, const double* traj /* Nall x J
     return s;
 }
 
+/* ---------------------------------------------------------------- orientation constraints
+ * OrientationConstraintEvaluator (constraint_evaluator.cpp:50-114) and the third-party
+ * arithmetic it reaches, restated from the published sources (not vendored; PARITY UNPINNED):
+ *   KDL Rotation::GetQuaternion (orocos KDL 1.0, frames.cpp; its non-trace branches evaluate
+ *     s in single precision, `float s = 2.0 * sqrtf(...)`),
+ *   tf::quaternionMsgToTF (normalises when |q|^2 is off by more than 0.1) and
+ *   btMatrix3x3::setRotation / inverse / operator* / getRPY -> getEulerYPR(solution 1)
+ *     (bullet LinearMath with BT_USE_DOUBLE_PRECISION, as built by ROS). */
+struct oc_eval {
+    int seg, body_fixed;
+    double ninv[9];        /* nominal_orientation_inverse_ */
+    double rw, pw, yw;     /* roll/pitch/yaw weights (0 when the tolerance is >= pi) */
+    double tol[3];         /* absolute roll / pitch / yaw tolerance */
+    double weight;
+};
+
+static void bt_from_quat(double x, double y, double z, double w, double* M)   /* btMatrix3x3::setRotation */
+{
+    const double d = x * x + y * y + z * z + w * w;
+    const double s = 2.0 / d;
+    const double xs = x * s, ys = y * s, zs = z * s;
+    const double wx = w * xs, wy = w * ys, wz = w * zs;
+    const double xx = x * xs, xy = x * ys, xz = x * zs;
+    const double yy = y * ys, yz = y * zs, zz = z * zs;
+    M[0] = 1.0 - (yy + zz); M[1] = xy - wz; M[2] = xz + wy;
+    M[3] = xy + wz; M[4] = 1.0 - (xx + zz); M[5] = yz - wx;
+    M[6] = xz - wy; M[7] = yz + wx; M[8] = 1.0 - (xx + yy);
+}
+
+static double bt_cofac(const double* M, int r1, int c1, int r2, int c2)
+{
+    return M[3 * r1 + c1] * M[3 * r2 + c2] - M[3 * r1 + c2] * M[3 * r2 + c1];
+}
+
+static void bt_inverse(const double* M, double* O)   /* btMatrix3x3::inverse */
+{
+    const double co0 = bt_cofac(M, 1, 1, 2, 2), co1 = bt_cofac(M, 1, 2, 2, 0), co2 = bt_cofac(M, 1, 0, 2, 1);
+    const double det = M[0] * co0 + M[1] * co1 + M[2] * co2;
+    const double s = 1.0 / det;
+    O[0] = co0 * s; O[1] = bt_cofac(M, 0, 2, 2, 1) * s; O[2] = bt_cofac(M, 0, 1, 1, 2) * s;
+    O[3] = co1 * s; O[4] = bt_cofac(M, 0, 0, 2, 2) * s; O[5] = bt_cofac(M, 0, 2, 1, 0) * s;
+    O[6] = co2 * s; O[7] = bt_cofac(M, 0, 1, 2, 0) * s; O[8] = bt_cofac(M, 0, 0, 1, 1) * s;
+}
+
+/* KDL Rotation::GetQuaternion (row-major R) */
+static void kdl_get_quaternion(const double* R, double* x, double* y, double* z, double* w)
+{
+    const double trace = R[0] + R[4] + R[8];
+    if (trace > 1e-12) {
+        const double s = 0.5 / sqrt(trace + 1.0);
+        *w = 0.25 / s;
+        *x = (R[7] - R[5]) * s;
+        *y = (R[2] - R[6]) * s;
+        *z = (R[3] - R[1]) * s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        const float s = (float)(2.0 * sqrtf((float)(1.0 + R[0] - R[4] - R[8])));
+        *w = (R[7] - R[5]) / s;
+        *x = 0.25 * s;
+        *y = (R[1] + R[3]) / s;
+        *z = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        const float s = (float)(2.0 * sqrtf((float)(1.0 + R[4] - R[0] - R[8])));
+        *w = (R[2] - R[6]) / s;
+        *x = (R[1] + R[3]) / s;
+        *y = 0.25 * s;
+        *z = (R[5] + R[7]) / s;
+    } else {
+        const float s = (float)(2.0 * sqrtf((float)(1.0 + R[8] - R[0] - R[4])));
+        *w = (R[3] - R[1]) / s;
+        *x = (R[2] + R[6]) / s;
+        *y = (R[5] + R[7]) / s;
+        *z = 0.25 * s;
+    }
+}
+
+/* btMatrix3x3::getRPY -> getEulerYPR(yaw, pitch, roll, 1) */
+static void bt_get_rpy(const double* M, double* roll, double* pitch, double* yaw)
+{
+    const double pi = 3.1415926535897932384626433832795029;
+    if (fabs(M[6]) >= 1.0) {
+        *yaw = 0.0;
+        const double delta = dm_atan2(M[0], M[2]);
+        if (M[6] > 0.0) {
+            *pitch = pi / 2.0;
+            *roll = *pitch + delta;
+        } else {
+            *pitch = -pi / 2.0;
+            *roll = -*pitch + delta;
+        }
+    } else {
+        double a = M[6];   /* btAsin clamps to [-1, 1] */
+        if (a < -1.0) a = -1.0;
+        if (a > 1.0) a = 1.0;
+        *pitch = -dm_asin(a);
+        double sp, cp;
+        dm_sincos(*pitch, &sp, &cp);
+        *roll = dm_atan2(M[7] / cp, M[8] / cp);
+        *yaw = dm_atan2(M[3] / cp, M[0] / cp);
+    }
+}
+
+static void bt_mul(const double* A, const double* B, double* C)   /* btMatrix3x3 operator* */
+{
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = A[3 * i + 0] * B[0 + j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+/* OrientationConstraintEvaluator ctor (constraint_evaluator.cpp:50-73) */
+static void oc_init(const so_orientation_constraint* c, struct oc_eval* o)
+{
+    double x = c->orientation[0], y = c->orientation[1], z = c->orientation[2], w = c->orientation[3];
+    const double l2 = x * x + y * y + z * z + w * w;
+    if (fabs(l2 - 1.0) > 0.1f) {   /* tf::quaternionMsgToTF: QUATERNION_TOLERANCE 0.1f */
+        const double inv = 1.0 / sqrt(l2);
+        x *= inv; y *= inv; z *= inv; w *= inv;
+    }
+    double nom[9];
+    bt_from_quat(x, y, z, w, nom);
+    bt_inverse(nom, o->ninv);
+    o->seg = c->segment;
+    o->body_fixed = c->body_fixed;
+    o->tol[0] = c->absolute_roll_tolerance;
+    o->tol[1] = c->absolute_pitch_tolerance;
+    o->tol[2] = c->absolute_yaw_tolerance;
+    o->weight = c->weight;
+    o->rw = o->pw = o->yw = 1.0;
+    if (o->tol[1] >= M_PI) o->pw = 0.0;
+    if (o->tol[0] >= M_PI) o->rw = 0.0;
+    if (o->tol[2] >= M_PI) o->yw = 0.0;
+}
+
+/* OrientationConstraintEvaluator::getCost (constraint_evaluator.cpp:80-114); returns satisfied */
+static int oc_cost(const struct oc_eval* o, const double* R, double* cost)
+{
+    double x, y, z, w, M[9], res[9], roll, pitch, yaw;
+    kdl_get_quaternion(R, &x, &y, &z, &w);
+    bt_from_quat(x, y, z, w, M);
+    if (!o->body_fixed) bt_mul(M, o->ninv, res);
+    else bt_mul(o->ninv, M, res);
+    bt_get_rpy(res, &roll, &pitch, &yaw);
+    roll = fabs(roll);
+    pitch = fabs(pitch);
+    yaw = fabs(yaw);
+    *cost = o->weight * (o->rw * roll + o->pw * pitch + o->yw * yaw);
+    return !(roll > o->tol[0] || pitch > o->tol[1] || yaw > o->tol[2]);
+}
+
 /* ---------------------------------------------------------------- distance field
  * distance_field::PropagationDistanceField::getDistanceGradient (3rd party; call site
  * stomp_collision_space.h:187-191): nearest cell = round((p - origin) * (1/res)) (VoxelGrid
@@ -507,7 +661,7 @@ void so_destroy(so_problem* P)
     free(P->tmp_params); free(P->tmp_noise); free(P->tmp_nproj); free(P->tmp_ctrl); free(P->tmp_prob);
     free(P->tmp_state);
     free(P->last_traj); free(P->best_traj);
-    free(P->chain); free(P->rb_m); free(P->rb_h); free(P->rb_I);
+    free(P->chain); free(P->rb_m); free(P->rb_h); free(P->rb_I); free(P->oc);
     free((void*)P->cfg.noise_stddev); free((void*)P->cfg.noise_decay);
     free((void*)P->cfg.start); free((void*)P->cfg.goal);
     free(P);
@@ -535,8 +689,8 @@ so_problem* so_create(const so_config* cfg)
         set_err("at most 32 joints");
         return NULL;
     }
-    if (cfg->num_orientation_constraints > 0) {
-        set_err("orientation constraints are not built yet");
+    if (cfg->num_orientation_constraints < 0 || (cfg->num_orientation_constraints > 0 && !cfg->orientation_constraints)) {
+        set_err("invalid orientation constraints");
         return NULL;
     }
     so_problem* P = (so_problem*)calloc(1, sizeof(so_problem));
@@ -611,6 +765,19 @@ so_problem* so_create(const so_config* cfg)
             rb_inertia(&cfg->inertias[P->chain[i]], &P->rb_m[i], P->rb_h + 3 * i, P->rb_I + 9 * i);
         }
     }
+
+    /* constraint_evaluators_ (stomp_optimizer.cpp:195-201) */
+    P->noc = cfg->num_orientation_constraints;
+    P->oc = (struct oc_eval*)calloc((size_t)(P->noc ? P->noc : 1), sizeof(struct oc_eval));
+    for (int c = 0; c < P->noc; ++c) {
+        if (cfg->orientation_constraints[c].segment < 0 || cfg->orientation_constraints[c].segment >= P->nseg) {
+            set_err("orientation constraint segment out of range");
+            so_destroy(P);
+            return NULL;
+        }
+        oc_init(&cfg->orientation_constraints[c], &P->oc[c]);
+    }
+    P->cfg.orientation_constraints = NULL;
 
     P->disc = cfg->discretization;
     /* group trajectory duration (N_all-1)*disc, truncated by getDuration() -> int
@@ -804,6 +971,7 @@ typedef struct {
     double* pot;      /* Nall x S */
     double* q;        /* J */
     frame_t* frames;  /* nseg */
+    double* con;      /* N: constraint cost per free waypoint */
 } exec_scratch;
 
 static void scratch_init(const so_problem* P, exec_scratch* s)
@@ -813,11 +981,12 @@ static void scratch_init(const so_problem* P, exec_scratch* s)
     s->pot = dalloc((size_t)P->Nall * (P->S ? P->S : 1));
     s->q = dalloc((size_t)P->J);
     s->frames = (frame_t*)malloc(sizeof(frame_t) * (size_t)P->nseg);
+    s->con = dalloc((size_t)P->N);
 }
 
 static void scratch_free(exec_scratch* s)
 {
-    free(s->traj); free(s->pos); free(s->pot); free(s->q); free(s->frames);
+    free(s->traj); free(s->pos); free(s->pot); free(s->q); free(s->frames); free(s->con);
 }
 
 /* StompOptimizer::handleJointLimits (stomp_optimizer.cpp:562-616) */
@@ -862,7 +1031,7 @@ static void handle_joint_limits(const so_problem* P, double* traj)
 }
 
 static void execute_one(const so_problem* P, exec_scratch* sc, const double* params, double* costs,
-                        int* collision_free, double* traj_out, int iteration_member, double* total)
+                        int* collision_free, double* traj_out, int iteration_member, double* total, int* cons_ok)
 {
     const int J = P->J, N = P->N, Nall = P->Nall, S = P->S;
     double* traj = sc->traj;
@@ -882,6 +1051,7 @@ static void execute_one(const so_problem* P, exec_scratch* sc, const double* par
 
     /* performForwardKinematics (stomp_optimizer.cpp:618-709) */
     int cf = !(iteration_member == 0 && P->pad_collision);
+    int cs = 1;   /* last_trajectory_constraints_satisfied_ (:1082) */
     memcpy(sc->pos, P->pad_pos, sizeof(double) * SO_PAD * S * 3);
     memcpy(sc->pos + (size_t)(SO_PAD + N) * S * 3, P->pad_pos + (size_t)SO_PAD * S * 3, sizeof(double) * SO_PAD * S * 3);
     for (int i = SO_PAD; i < SO_PAD + N; ++i) {
@@ -889,6 +1059,14 @@ static void execute_one(const so_problem* P, exec_scratch* sc, const double* par
         fk_spheres(P, sc->q, sc->frames, sc->pos + (size_t)i * S * 3);
         for (int j = 0; j < S; ++j)
             if (potential_of(P, j, sc->pos + ((size_t)i * S + j) * 3, &sc->pot[(size_t)i * S + j])) cf = 0;
+        /* constraint evaluators on the waypoint's segment frames (stomp_optimizer.cpp:1107-1115) */
+        double con = 0.0;
+        for (int c = 0; c < P->noc; ++c) {
+            double cc;
+            if (!oc_cost(&P->oc[c], sc->frames[P->oc[c].seg].R, &cc)) cs = 0;
+            con += cc;
+        }
+        sc->con[i - SO_PAD] = con;
     }
     const double invTime = 1.0 / P->disc;
     double sum = 0.0;
@@ -910,22 +1088,23 @@ static void execute_one(const so_problem* P, exec_scratch* sc, const double* par
         }
         /* stomp_optimizer.cpp:1117-1151 */
         const double tq = P->torque ? torque_cost_at(P, traj, i) : 0.0;
-        double c = P->cfg.obstacle_cost_weight * state + P->cfg.constraint_cost_weight * 0.0 +
+        double c = P->cfg.obstacle_cost_weight * state + P->cfg.constraint_cost_weight * sc->con[i - SO_PAD] +
                    P->cfg.torque_cost_weight * tq;
         costs[i - SO_PAD] = c;
     }
     for (int t = 0; t < N; ++t) sum = (t == 0) ? costs[0] : sum + costs[t];   /* costs.sum() :1155 */
     *collision_free = cf;
+    if (cons_ok) *cons_ok = cs;
     if (total) *total = sum;
 }
 
 int so_execute(so_problem* P, const double* params, double* costs, int* collision_free, double* traj_out,
-               int iteration_member)
+               int iteration_member, int* constraints_ok)
 {
     exec_scratch sc;
     scratch_init(P, &sc);
     double tot;
-    execute_one(P, &sc, params, costs, collision_free, traj_out, iteration_member, &tot);
+    execute_one(P, &sc, params, costs, collision_free, traj_out, iteration_member, &tot, constraints_ok);
     scratch_free(&sc);
     return 0;
 }
@@ -1158,7 +1337,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
 #endif
         for (int r = 0; r < P->K_gen; ++r) {
             int cf;
-            execute_one(P, &sc, P->r_params + r * JN, P->r_state + (size_t)r * N, &cf, NULL, iteration_member, NULL);
+            execute_one(P, &sc, P->r_params + r * JN, P->r_state + (size_t)r * N, &cf, NULL, iteration_member, NULL, NULL);
         }
         scratch_free(&sc);
     }
@@ -1216,7 +1395,8 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
     {
         exec_scratch sc;
         scratch_init(P, &sc);
-        execute_one(P, &sc, P->theta, P->x_state, &P->last_cf, P->last_traj, iteration_member, &P->last_cost);
+        execute_one(P, &sc, P->theta, P->x_state, &P->last_cf, P->last_traj, iteration_member, &P->last_cost,
+                    &P->last_cs);
         scratch_free(&sc);
         /* addExtraRollouts (policy_improvement.cpp:443-462) */
         memcpy(P->x_params, P->theta, JN * 8);
@@ -1232,6 +1412,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
     if (out) {
         out->cost = P->last_cost;
         out->collision_free = P->last_cf;
+        out->constraints_satisfied = P->last_cs;
     }
     return 0;
 }
@@ -1251,10 +1432,12 @@ int so_optimize(so_problem* P, so_stats* st, double* costs_per_it)
     for (it = 0; it < P->cfg.max_iterations; it++) {
         so_iter_out o;
         so_iterate(P, it + 1, &o);
-        if (o.collision_free) cfi++;
+        /* stomp_optimizer.cpp:301-339 */
+        const int ok = o.collision_free && o.constraints_satisfied;
+        if (ok) cfi++;
         else cfi = 0;
         if (o.collision_free && s.collision_success_iteration == -1) s.collision_success_iteration = it;
-        if (o.collision_free && s.success_iteration == -1) {
+        if (ok && s.success_iteration == -1) {
             s.success_iteration = it;
             s.success = 1;
         }
@@ -1263,7 +1446,7 @@ int so_optimize(so_problem* P, so_stats* st, double* costs_per_it)
         if (it == 0) {
             memcpy(P->best_traj, P->last_traj, JN * 8);
             best_cost = cost;
-        } else if (cost < best_cost && o.collision_free) {
+        } else if (cost < best_cost && ok) {
             memcpy(P->best_traj, P->last_traj, JN * 8);
             best_cost = cost;
             s.last_improvement_iteration = it;

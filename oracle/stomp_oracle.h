@@ -131,9 +131,12 @@ typedef struct so_problem so_problem;
 typedef struct {
     double cost;                /* last_trajectory_cost_ of the noiseless rollout */
     int collision_free;         /* last_trajectory_collision_free_ */
+    int constraints_satisfied;  /* last_trajectory_constraints_satisfied_ */
 } so_iter_out;
 
 /* KDL::ChainIdSolver_RNE::CartToJnt on the torque chain, group joint vectors of length J */
+double so_atan2(double y, double x);
+double so_asin(double x);
 int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, const double* qdd, double* tau);
 
 typedef struct {
@@ -158,7 +161,8 @@ int so_get_pad_positions(const so_problem* p, double* out /* 12 x S x 3 */);
 /* Task::execute on one parameter set (J x N, row per joint). iteration_member is the
  * optimizer's iteration_ (0 => padding points count toward the collision flag). */
 int so_execute(so_problem* p, const double* params, double* costs, int* collision_free,
-               double* traj_out /* J x N clamped free block, may be NULL */, int iteration_member);
+               double* traj_out /* J x N clamped free block, may be NULL */, int iteration_member,
+               int* constraints_ok /* last_trajectory_constraints_satisfied_, may be NULL */);
 
 /* runSingleIteration(iteration_number); the optimizer's iteration_ is iteration_number-1 */
 int so_iterate(so_problem* p, int iteration_number, so_iter_out* out);

@@ -54,6 +54,7 @@ struct stomp_engine {
     TermsModel terms{};
     bool terms_on = false;      // torque term / path constraints: k_terms after every k_rollout
     double* d_terms_traj = nullptr;   // [K_loc][J][N] joint-limited trajectories for k_terms
+    uint8_t* d_cs = nullptr;          // last_trajectory_constraints_satisfied_ of the noiseless rollout
     std::vector<FkOp> ops;
     std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
     int nslots = 0;
@@ -79,6 +80,7 @@ struct stomp_engine {
     int eval_cap = 0;
     double *d_eval_params = nullptr, *d_eval_costs = nullptr, *d_eval_traj = nullptr;
     uint8_t* d_eval_cf = nullptr;
+    uint8_t* d_eval_cs = nullptr;
     // timing
     bool timing = false;
     struct Ev {
@@ -272,6 +274,34 @@ const char* torque_chain(const stomp_engine_desc* d, std::vector<int>& path)
     return nullptr;
 }
 
+// OrientationConstraintEvaluator ctor (constraint_evaluator.cpp:50-73): tf::quaternionMsgToTF
+// (normalises when |q|^2 is off by more than 0.1), btMatrix3x3(btQuaternion), inverse()
+// (bullet LinearMath, double precision), restated as in the oracle
+void oc_nominal_inverse(const double* q, double* O)
+{
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double l2 = x * x + y * y + z * z + w * w;
+    if (std::fabs(l2 - 1.0) > 0.1f) {
+        const double inv = 1.0 / std::sqrt(l2);
+        x *= inv; y *= inv; z *= inv; w *= inv;
+    }
+    const double d = x * x + y * y + z * z + w * w;
+    const double s = 2.0 / d;
+    const double xs = x * s, ys = y * s, zs = z * s;
+    const double wx = w * xs, wy = w * ys, wz = w * zs;
+    const double xx = x * xs, xy = x * ys, xz = x * zs;
+    const double yy = y * ys, yz = y * zs, zz = z * zs;
+    const double M[9] = {1.0 - (yy + zz), xy - wz, xz + wy, xy + wz, 1.0 - (xx + zz), yz - wx,
+                         xz - wy, yz + wx, 1.0 - (xx + yy)};
+    auto cof = [&](int r1, int c1, int r2, int c2) { return M[3 * r1 + c1] * M[3 * r2 + c2] - M[3 * r1 + c2] * M[3 * r2 + c1]; };
+    const double co0 = cof(1, 1, 2, 2), co1 = cof(1, 2, 2, 0), co2 = cof(1, 0, 2, 1);
+    const double det = M[0] * co0 + M[1] * co1 + M[2] * co2;
+    const double sc = 1.0 / det;
+    O[0] = co0 * sc; O[1] = cof(0, 2, 2, 1) * sc; O[2] = cof(0, 1, 1, 2) * sc;
+    O[3] = co1 * sc; O[4] = cof(0, 0, 2, 2) * sc; O[5] = cof(0, 2, 1, 0) * sc;
+    O[6] = co2 * sc; O[7] = cof(0, 1, 2, 0) * sc; O[8] = cof(0, 0, 1, 1) * sc;
+}
+
 void release(stomp_engine* e)
 {
     if (!e) return;
@@ -289,14 +319,15 @@ void release(stomp_engine* e)
 
 // the state-cost terms after the collision cost (k_terms), on the rollouts a k_rollout
 // launch with these arguments evaluated; its trajectories must have been written
-void launch_terms_for(stomp_engine* e, const CostArgs& ca)
+void launch_terms_for(stomp_engine* e, const CostArgs& ca, uint8_t* cs = nullptr)
 {
     if (!e->terms_on) return;
     Timed tm(e, T_TERMS);
     TermsArgs ta{};
     ta.traj = ca.traj_out; ta.state = ca.state_out; ta.total = ca.total_out; ta.num_noisy = ca.num_noisy;
+    ta.cs = cs;
     if (ca.x_params) {
-        ta.x_traj = ca.x_traj; ta.x_state = ca.x_state; ta.x_total = ca.x_total;
+        ta.x_traj = ca.x_traj; ta.x_state = ca.x_state; ta.x_total = ca.x_total; ta.x_cs = e->d_cs;
     }
     launch_terms(e->terms, ta, e->stream);
 }
@@ -485,8 +516,11 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (d->num_rollouts <= 0) return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be positive");
     if (d->num_reused_rollouts < 0 || d->num_reused_rollouts >= d->num_rollouts)
         return fail(nullptr, STOMP_E_INVALID, "Number of reused rollouts must be strictly less than number of rollouts.");
-    if (d->num_orientation_constraints > 0)
-        return fail(nullptr, STOMP_E_UNSUPPORTED, "orientation constraints are not built yet");
+    if (d->num_orientation_constraints < 0 || (d->num_orientation_constraints > 0 && !d->orientation_constraints))
+        return fail(nullptr, STOMP_E_INVALID, "invalid orientation constraints");
+    for (int c = 0; c < d->num_orientation_constraints; ++c)
+        if (d->orientation_constraints[c].segment < 0 || d->orientation_constraints[c].segment >= d->num_segments)
+            return fail(nullptr, STOMP_E_INVALID, "orientation constraint %d: bad segment", c);
     if (d->num_segments <= 0 || !d->segments || (d->num_spheres > 0 && !d->spheres) || !d->joints || !d->noise_stddev ||
         !d->noise_decay || !d->start || !d->goal || !d->grid.data)
         return fail(nullptr, STOMP_E_INVALID, "missing table pointer");
@@ -651,6 +685,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_best_traj, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_total, 1));
     CREATE_TRY(dev_alloc(e, &e->d_cf, 1));
+    CREATE_TRY(dev_alloc(e, &e->d_cs, 1));
+    if (hipMemsetAsync(e->d_cs, 1, 1, e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
     CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
@@ -685,6 +721,32 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         t.nchain = (int)cs.size();
         t.chain = d_chain;
         for (int k = 0; k < 3; ++k) t.g[k] = d->gravity[k];
+        e->terms_on = true;
+    }
+    if (d->num_orientation_constraints > 0) {
+        std::vector<OcDev> oc(d->num_orientation_constraints);
+        for (int c = 0; c < d->num_orientation_constraints; ++c) {
+            const stomp_orientation_constraint& in = d->orientation_constraints[c];
+            OcDev& o = oc[c];
+            std::vector<int> path;
+            for (int sgi = in.segment; sgi >= 0; sgi = d->segments[sgi].parent) path.push_back(sgi);
+            if ((int)path.size() > kMaxChain)
+                CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "constraint segment deeper than %d", kMaxChain));
+            std::reverse(path.begin(), path.end());
+            o.seg = in.segment; o.body_fixed = in.body_fixed ? 1 : 0; o.path_len = (int)path.size();
+            for (size_t k = 0; k < path.size(); ++k) o.path[k] = path[k];
+            oc_nominal_inverse(in.orientation, o.ninv);
+            o.tol[0] = in.absolute_roll_tolerance; o.tol[1] = in.absolute_pitch_tolerance;
+            o.tol[2] = in.absolute_yaw_tolerance; o.weight = in.weight;
+            o.rw = o.pw = o.yw = 1.0;   // constraint_evaluator.cpp:66-72
+            if (o.tol[1] >= M_PI) o.pw = 0.0;
+            if (o.tol[0] >= M_PI) o.rw = 0.0;
+            if (o.tol[2] >= M_PI) o.yw = 0.0;
+        }
+        OcDev* d_oc;
+        CREATE_TRY(upload(e, &d_oc, oc.data(), oc.size()));
+        e->terms.noc = (int)oc.size();
+        e->terms.oc = d_oc;
         e->terms_on = true;
     }
     if (e->terms_on) {
@@ -760,6 +822,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         e->d_pad_pos = (double*)(base + (L.pad - L.sph));
     }
     m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
+    e->terms.segs = m.segs;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
     m.inv_res = 1.0 / d->grid.resolution;
@@ -824,10 +887,12 @@ int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
     if (rc) return rc;
     HIP_TRY(e, hipMemcpyAsync(e->h_total, e->d_total, sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(e->h_cf, e->d_cf, 1, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->h_cf + 1, e->d_cs, 1, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     if (out) {
         out->cost = *e->h_total;
         out->collision_free = e->h_cf[0];
+        out->constraints_satisfied = e->h_cf[1];
     }
     return 0;
 }
@@ -849,12 +914,13 @@ int stomp_engine_synchronize(stomp_engine* e)
 }
 
 int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double* costs, uint8_t* collision_free,
-                      double* traj_out, int32_t iteration_member)
+                      double* traj_out, int32_t iteration_member, uint8_t* constraints_satisfied)
 {
     if (num <= 0) return 0;
     const size_t JN = (size_t)e->J * e->N;
     if (num > e->eval_cap) {
-        for (void* p : {(void*)e->d_eval_params, (void*)e->d_eval_costs, (void*)e->d_eval_traj, (void*)e->d_eval_cf}) {
+        for (void* p : {(void*)e->d_eval_params, (void*)e->d_eval_costs, (void*)e->d_eval_traj, (void*)e->d_eval_cf,
+                        (void*)e->d_eval_cs}) {
             if (!p) continue;
             hipFree(p);
             e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), p), e->allocs.end());
@@ -864,6 +930,7 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
         if ((rc = dev_alloc(e, &e->d_eval_costs, (size_t)num * e->N))) return rc;
         if ((rc = dev_alloc(e, &e->d_eval_traj, num * JN))) return rc;
         if ((rc = dev_alloc(e, &e->d_eval_cf, (size_t)num))) return rc;
+        if ((rc = dev_alloc(e, &e->d_eval_cs, (size_t)num))) return rc;
         e->eval_cap = num;
     }
     HIP_TRY(e, hipMemcpyAsync(e->d_eval_params, params, sizeof(double) * num * JN, hipMemcpyHostToDevice, e->stream));
@@ -872,11 +939,14 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
     ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf;
     ca.traj_out = (traj_out || e->terms_on) ? e->d_eval_traj : nullptr;
     launch_cost(e->model, ca, e->stream);
-    launch_terms_for(e, ca);
+    if (constraints_satisfied && !e->terms_on) HIP_TRY(e, hipMemsetAsync(e->d_eval_cs, 1, (size_t)num, e->stream));
+    launch_terms_for(e, ca, e->d_eval_cs);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipMemcpyAsync(costs, e->d_eval_costs, sizeof(double) * num * e->N, hipMemcpyDeviceToHost, e->stream));
     if (collision_free)
         HIP_TRY(e, hipMemcpyAsync(collision_free, e->d_eval_cf, num, hipMemcpyDeviceToHost, e->stream));
+    if (constraints_satisfied)
+        HIP_TRY(e, hipMemcpyAsync(constraints_satisfied, e->d_eval_cs, num, hipMemcpyDeviceToHost, e->stream));
     if (traj_out)
         HIP_TRY(e, hipMemcpyAsync(traj_out, e->d_eval_traj, sizeof(double) * num * JN, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -898,15 +968,16 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
         stomp_iter_out o;
         int rc = stomp_engine_iterate(e, it + 1, &o);
         if (rc) return rc;
-        if (o.collision_free) cfi++;
+        const bool ok = o.collision_free && o.constraints_satisfied;   // stomp_optimizer.cpp:301-339
+        if (ok) cfi++;
         else cfi = 0;
         if (o.collision_free && s.collision_success_iteration == -1) s.collision_success_iteration = it;
-        if (o.collision_free && s.success_iteration == -1) {
+        if (ok && s.success_iteration == -1) {
             s.success_iteration = it;
             s.success = 1;
         }
         if (costs_per_it) costs_per_it[it] = o.cost;
-        if (it == 0 || (o.cost < best && o.collision_free)) {
+        if (it == 0 || (o.cost < best && ok)) {
             HIP_TRY(e, hipMemcpyAsync(e->d_best_traj, e->d_last_traj, bytes, hipMemcpyDeviceToDevice, e->stream));
             best = o.cost;
             if (it != 0) s.last_improvement_iteration = it;

@@ -1,6 +1,9 @@
 // k_terms.hip -- the state-cost terms StompOptimizer::execute adds after the collision cost
 // (stomp_optimizer.cpp:1107-1151), one workgroup per rollout, lane t = free waypoint t.
 //
+// Orientation constraints (:1107-1115): the FK frame of the constrained segment along its
+// root-first path, then OrientationConstraintEvaluator::getCost (constraint_evaluator.cpp:80-114)
+// with KDL's GetQuaternion and bullet's setRotation / getRPY restated as in the oracle.
 // Torque term (:1117-1142, StompOptimizer::getTorques :1033-1061): q at row t of the
 // joint-limited group trajectory, q-dot / q-ddot by the 7-tap rules of
 // StompTrajectory::getJointVelocities / getJointAccelerations (stomp_trajectory.h:286-310),
@@ -68,6 +71,93 @@ __device__ __forceinline__ void rbi_mul(const ChainSeg& c, const Twist& t, doubl
     }
 }
 
+// btMatrix3x3::setRotation(btQuaternion) (bullet LinearMath, double precision)
+__device__ __forceinline__ void bt_from_quat(double x, double y, double z, double w, double* M)
+{
+    const double d = x * x + y * y + z * z + w * w;
+    const double s = 2.0 / d;
+    const double xs = x * s, ys = y * s, zs = z * s;
+    const double wx = w * xs, wy = w * ys, wz = w * zs;
+    const double xx = x * xs, xy = x * ys, xz = x * zs;
+    const double yy = y * ys, yz = y * zs, zz = z * zs;
+    M[0] = 1.0 - (yy + zz); M[1] = xy - wz; M[2] = xz + wy;
+    M[3] = xy + wz; M[4] = 1.0 - (xx + zz); M[5] = yz - wx;
+    M[6] = xz - wy; M[7] = yz + wx; M[8] = 1.0 - (xx + yy);
+}
+
+// KDL Rotation::GetQuaternion (orocos KDL 1.0): the non-trace branches compute s in single
+// precision (`float s = 2.0 * sqrtf(...)`)
+__device__ __forceinline__ void kdl_quat(const double* R, double* x, double* y, double* z, double* w)
+{
+    const double trace = R[0] + R[4] + R[8];
+    if (trace > 1e-12) {
+        const double s = 0.5 / sqrt(trace + 1.0);
+        *w = 0.25 / s;
+        *x = (R[7] - R[5]) * s;
+        *y = (R[2] - R[6]) * s;
+        *z = (R[3] - R[1]) * s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        const float s = (float)(2.0 * (double)__builtin_sqrtf((float)(1.0 + R[0] - R[4] - R[8])));
+        *w = (R[7] - R[5]) / (double)s;
+        *x = 0.25 * (double)s;
+        *y = (R[1] + R[3]) / (double)s;
+        *z = (R[2] + R[6]) / (double)s;
+    } else if (R[4] > R[8]) {
+        const float s = (float)(2.0 * (double)__builtin_sqrtf((float)(1.0 + R[4] - R[0] - R[8])));
+        *w = (R[2] - R[6]) / (double)s;
+        *x = (R[1] + R[3]) / (double)s;
+        *y = 0.25 * (double)s;
+        *z = (R[5] + R[7]) / (double)s;
+    } else {
+        const float s = (float)(2.0 * (double)__builtin_sqrtf((float)(1.0 + R[8] - R[0] - R[4])));
+        *w = (R[3] - R[1]) / (double)s;
+        *x = (R[2] + R[6]) / (double)s;
+        *y = (R[5] + R[7]) / (double)s;
+        *z = 0.25 * (double)s;
+    }
+}
+
+// OrientationConstraintEvaluator::getCost (constraint_evaluator.cpp:80-114) on the segment
+// rotation R; returns satisfied
+__device__ bool oc_cost(const OcDev& o, const double* R, double* cost)
+{
+    double x, y, z, w, M[9], E[9];
+    kdl_quat(R, &x, &y, &z, &w);
+    bt_from_quat(x, y, z, w, M);
+    const double* A = o.body_fixed ? o.ninv : M;   // header frame: M N^-1; body fixed: N^-1 M
+    const double* B = o.body_fixed ? M : o.ninv;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            E[3 * i + j] = A[3 * i + 0] * B[0 + j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    // btMatrix3x3::getRPY -> getEulerYPR(solution 1)
+    const double pi = 3.1415926535897932384626433832795029;
+    double roll, pitch, yaw;
+    if (fabs(E[6]) >= 1.0) {
+        yaw = 0.0;
+        const double delta = det_atan2(E[0], E[2]);
+        if (E[6] > 0.0) {
+            pitch = pi / 2.0;
+            roll = pitch + delta;
+        } else {
+            pitch = -pi / 2.0;
+            roll = -pitch + delta;
+        }
+    } else {
+        pitch = -det_asin(E[6]);
+        double sp, cp;
+        det_sincos(pitch, &sp, &cp);
+        roll = det_atan2(E[7] / cp, E[8] / cp);
+        yaw = det_atan2(E[3] / cp, E[0] / cp);
+    }
+    roll = fabs(roll);
+    pitch = fabs(pitch);
+    yaw = fabs(yaw);
+    *cost = o.weight * (o.rw * roll + o.pw * pitch + o.yw * yaw);
+    return !(roll > o.tol[0] || pitch > o.tol[1] || yaw > o.tol[2]);
+}
+
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
 {
@@ -80,6 +170,7 @@ __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
     const double* traj = extra ? a.x_traj : a.traj + (long long)e * J * N;
     double* state = extra ? a.x_state : a.state + (long long)e * N;
     double* total = extra ? a.x_total : (a.total ? a.total + e : nullptr);
+    uint8_t* cso = extra ? a.x_cs : (a.cs ? a.cs + e : nullptr);
 
     // q, q-dot, q-ddot for every (joint, waypoint): padding rows are start / goal
     for (int idx = t; idx < J * N; idx += BLOCK) {
@@ -101,6 +192,29 @@ __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
         Q[2 * J * N + idx] = qdd;
     }
     __syncthreads();
+
+    // orientation constraints on the waypoint's FK frames (stomp_optimizer.cpp:1107-1115); the
+    // segment frame is composed root-first along its path, as the FK of every segment does
+    double con = 0.0;
+    int ok = 1;
+    if (t < N) {
+        for (int c = 0; c < m.noc; ++c) {
+            const OcDev& o = m.oc[c];
+            Frame Fr;
+            for (int k = 0; k < o.path_len; ++k) {
+                const DevSegment& sg = m.segs[o.path[k]];
+                double st = 0.0, ct = 1.0;
+                if (sg.q_index >= 0) det_sincos(Q[sg.q_index * N + t], &st, &ct);
+                Frame nf;
+                compose(sg, k == 0 ? nullptr : &Fr, st, ct, nf);
+                Fr = nf;
+            }
+            double cc;
+            if (!oc_cost(o, Fr.R, &cc)) ok = 0;
+            con += cc;
+        }
+    }
+    const int all_ok = __syncthreads_and(ok);
 
     double tq = 0.0;
     if (t < N && m.torque) {
@@ -195,7 +309,7 @@ __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
     __syncthreads();
     double* cst = F;   // the costs, for the total
     if (t < N) {
-        const double c = (state[t] + m.w_con * 0.0) + m.w_tq * tq;
+        const double c = (state[t] + m.w_con * con) + m.w_tq * tq;
         state[t] = c;
         cst[t] = c;
     }
@@ -205,6 +319,7 @@ __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
         for (int k = 0; k < N; ++k) s += cst[k];
         *total = s;
     }
+    if (t == 0 && cso) *cso = all_ok ? 1 : 0;
 }
 
 }  // namespace

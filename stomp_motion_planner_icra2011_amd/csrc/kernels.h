@@ -177,8 +177,8 @@ struct WeightArgs {
 };
 
 // The state-cost terms that StompOptimizer::execute adds after the collision cost
-// (stomp_optimizer.cpp:1107-1151): the torque term (KDL::ChainIdSolver_RNE on the
-// inverse-dynamics chain, :1117-1142).  k_terms runs after k_rollout on the same rollouts,
+// (stomp_optimizer.cpp:1107-1151): the orientation path constraints (:1107-1115) and the
+// torque term (KDL::ChainIdSolver_RNE on the inverse-dynamics chain, :1117-1142).  k_terms runs after k_rollout on the same rollouts,
 // reading the joint-limited trajectories k_rollout wrote, and finishes
 // costs(t) = (w_obs state + w_con con) + w_tq tq in the reference's order.
 constexpr int kMaxChain = 32;
@@ -188,9 +188,22 @@ struct ChainSeg {
     double m, h[3], I[9];       // KDL::RigidBodyInertia about the segment origin (h = m c)
 };
 
+// OrientationConstraintEvaluator (constraint_evaluator.cpp:50-73) with the FK path of its
+// segment (root first), for one lane per waypoint
+struct OcDev {
+    int seg, body_fixed, path_len;
+    int path[kMaxChain];
+    double ninv[9];             // nominal_orientation_inverse_ (bullet inverse, host-computed)
+    double rw, pw, yw;          // roll / pitch / yaw weights
+    double tol[3];              // absolute roll / pitch / yaw tolerance
+    double weight;
+};
+
 struct TermsModel {
-    int J, N, nchain, torque;
+    int J, N, nchain, torque, noc;
     const ChainSeg* chain;      // [nchain], root side first
+    const OcDev* oc;            // [noc]
+    const DevSegment* segs;     // the whole tree (constraint FK paths)
     double g[3];                // gravity in the chain root frame
     double cv[7], ca[7];        // invTime * DIFF_RULES[0][k], invTime^2 * DIFF_RULES[1][k]
     const double* start;        // [J]
@@ -203,9 +216,11 @@ struct TermsArgs {
     double* state;              // [num_noisy][N] in: w_obs * collision cost; out: the full costs
     double* total;              // [num_noisy] or null
     int num_noisy;
+    uint8_t* cs;                // [num_noisy] constraints satisfied, or null
     const double* x_traj;       // the extra (noiseless) rollout, or null
     double* x_state;
     double* x_total;
+    uint8_t* x_cs;
 };
 
 size_t terms_lds_bytes(const TermsModel& m);

@@ -120,6 +120,125 @@ STOMP_HD void det_sincos(double x, double* s, double* c)
     *c = co;
 }
 
+// atan: fdlibm s_atan.c (reduction about atan(0.5), atan(1), atan(1.5), atan(inf), hi/lo
+// constants, odd/even minimax polynomial)
+STOMP_HD double det_atan(double x)
+{
+    const double hi0 = 4.63647609000806093515e-01, hi1 = 7.85398163397448278999e-01,
+                 hi2 = 9.82793723247329054082e-01, hi3 = 1.57079632679489655800e+00;
+    const double lo0 = 2.26987774529616870924e-17, lo1 = 3.06161699786838301793e-17,
+                 lo2 = 1.39033110312309984516e-17, lo3 = 6.12323399573676603587e-17;
+    const double a0 = 3.33333333333329318027e-01, a1 = -1.99999999998764832476e-01,
+                 a2 = 1.42857142725034663711e-01, a3 = -1.11111104054623557880e-01,
+                 a4 = 9.09088713343650656196e-02, a5 = -7.69187620504482999495e-02,
+                 a6 = 6.66107313738753120669e-02, a7 = -5.83357013379057348645e-02,
+                 a8 = 4.97687799461593236017e-02, a9 = -3.65315727442169155270e-02,
+                 a10 = 1.62858201153657823623e-02;
+    const int hx = (int)(double_to_bits(x) >> 32);
+    const int ix = hx & 0x7fffffff;
+    if (ix >= 0x44100000) {
+        if (x != x) return x + x;
+        return hx > 0 ? hi3 + lo3 : -hi3 - lo3;
+    }
+    int id = -1;
+    if (ix < 0x3fdc0000) {
+        if (ix < 0x3e400000) return x;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else {
+            if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+            else { id = 3; x = -1.0 / x; }
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (a0 + w * (a2 + w * (a4 + w * (a6 + w * (a8 + w * a10)))));
+    const double s2 = w * (a1 + w * (a3 + w * (a5 + w * (a7 + w * a9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double hi = id == 0 ? hi0 : (id == 1 ? hi1 : (id == 2 ? hi2 : hi3));
+    const double lo = id == 0 ? lo0 : (id == 1 ? lo1 : (id == 2 ? lo2 : lo3));
+    const double r = hi - ((x * (s1 + s2) - lo) - x);
+    return hx < 0 ? -r : r;
+}
+
+// atan2: fdlibm e_atan2.c
+STOMP_HD double det_atan2(double y, double x)
+{
+    const double pi_o_4 = 7.8539816339744827900E-01, pi_o_2 = 1.5707963267948965580E+00,
+                 pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    if (x != x || y != y) return x + y;
+    const uint64_t ux = double_to_bits(x), uy = double_to_bits(y);
+    const int hx = (int)(ux >> 32), hy = (int)(uy >> 32);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const unsigned lx = (unsigned)ux, ly = (unsigned)uy;
+    if (x == 1.0) return det_atan(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if ((iy | ly) == 0) return m <= 1 ? y : (m == 2 ? pi : -pi);
+    if ((ix | lx) == 0) return hy < 0 ? -pi_o_2 : pi_o_2;
+    if (ix == 0x7ff00000) {
+        if (iy == 0x7ff00000)
+            return m == 0 ? pi_o_4 : (m == 1 ? -pi_o_4 : (m == 2 ? 3.0 * pi_o_4 : -3.0 * pi_o_4));
+        return m == 0 ? 0.0 : (m == 1 ? -0.0 : (m == 2 ? pi : -pi));
+    }
+    if (iy == 0x7ff00000) return hy < 0 ? -pi_o_2 : pi_o_2;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = pi_o_2 + 0.5 * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = det_atan(fabs(y / x));
+    if (m == 0) return z;
+    if (m == 1) return -z;
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
+
+// asin: fdlibm e_asin.c
+STOMP_HD double det_asin(double x)
+{
+    const double pio2_hi = 1.57079632679489655800e+00, pio2_lo = 6.12323399573676603587e-17,
+                 pio4_hi = 7.85398163397448278999e-01;
+    const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
+                 pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
+                 pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05;
+    const double qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
+                 qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+    const uint64_t u = double_to_bits(x);
+    const int hx = (int)(u >> 32);
+    const int ix = hx & 0x7fffffff;
+    if (ix >= 0x3ff00000) {
+        if (((ix - 0x3ff00000) | (unsigned)u) == 0) return x * pio2_hi + x * pio2_lo;
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3fe00000) {
+        if (ix < 0x3e400000) return x;
+        const double t = x * x;
+        const double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+        const double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+        const double w = p / q;
+        return x + x * w;
+    }
+    const double w0 = 1.0 - fabs(x);
+    double t = w0 * 0.5;
+    double p = t * (pS0 + t * (pS1 + t * (pS2 + t * (pS3 + t * (pS4 + t * pS5)))));
+    double q = 1.0 + t * (qS1 + t * (qS2 + t * (qS3 + t * qS4)));
+    const double s = sqrt(t);
+    if (ix >= 0x3FEF3333) {
+        const double w = p / q;
+        t = pio2_hi - (2.0 * (s + s * w) - pio2_lo);
+    } else {
+        const double w = bits_to_double(double_to_bits(s) & 0xFFFFFFFF00000000ull);
+        const double c = (t - w * w) / (s + w);
+        const double r = p / q;
+        p = 2.0 * s * r - (pio2_lo - 2.0 * c);
+        q = pio4_hi - 2.0 * w;
+        t = pio4_hi - (p - q);
+    }
+    return hx > 0 ? t : -t;
+}
+
 // Philox4x32-10 (Salmon et al., SC'11)
 STOMP_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                             uint32_t out[4])

@@ -64,7 +64,7 @@ class stomp_engine_desc(C.Structure):
 
 
 class stomp_iter_out(C.Structure):
-    _fields_ = [("cost", C.c_double), ("collision_free", C.c_int32)]
+    _fields_ = [("cost", C.c_double), ("collision_free", C.c_int32), ("constraints_satisfied", C.c_int32)]
 
 
 class stomp_stats(C.Structure):
@@ -109,7 +109,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_iterate.argtypes = [P, C.c_int32, C.POINTER(stomp_iter_out)]
     l.stomp_engine_run.argtypes = [P, C.c_int32, C.c_int32]
     l.stomp_engine_synchronize.argtypes = [P]
-    l.stomp_engine_eval.argtypes = [P, dp, C.c_int32, dp, C.POINTER(C.c_uint8), dp, C.c_int32]
+    l.stomp_engine_eval.argtypes = [P, dp, C.c_int32, dp, C.POINTER(C.c_uint8), dp, C.c_int32, C.POINTER(C.c_uint8)]
     l.stomp_engine_optimize.argtypes = [P, C.POINTER(stomp_stats), dp]
     l.stomp_engine_get_best_trajectory.argtypes = [P, dp]
     l.stomp_engine_get_last_trajectory.argtypes = [P, dp]
@@ -263,6 +263,7 @@ class Engine:
     def iterate(self, iteration_number: int):
         o = stomp_iter_out()
         _check(load_library().stomp_engine_iterate(self.h, iteration_number, C.byref(o)), self.h)
+        self.last_constraints_satisfied = bool(o.constraints_satisfied)
         return o.cost, bool(o.collision_free)
 
     def run(self, first_iteration: int, count: int):
@@ -279,8 +280,11 @@ class Engine:
         costs = np.zeros((n, self.N))
         cf = np.zeros(n, np.uint8)
         traj = np.zeros((n, self.J, self.N))
-        _check(load_library().stomp_engine_eval(self.h, _dp(prm), n, _dp(costs), cf.ctypes.data_as(C.POINTER(C.c_uint8)),
-                                                _dp(traj), iteration_member), self.h)
+        cs = np.zeros(n, np.uint8)
+        u8 = C.POINTER(C.c_uint8)
+        _check(load_library().stomp_engine_eval(self.h, _dp(prm), n, _dp(costs), cf.ctypes.data_as(u8), _dp(traj),
+                                                iteration_member, cs.ctypes.data_as(u8)), self.h)
+        self.last_constraints_satisfied = cs.astype(bool)
         if single:
             return costs[0], bool(cf[0]), traj[0]
         return costs, cf.astype(bool), traj

@@ -18,8 +18,8 @@ std::string engine_error(stomp_engine* e, int rc)
 // ------------------------------------------------------------------ StompOptimizer
 
 StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model,
-                               const StompParameters* parameters, StompCollisionSpace* collision_space, int device,
-                               void* stream)
+                               const StompParameters* parameters, StompCollisionSpace* collision_space,
+                               const Constraints& constraints, int device, void* stream)
     : trajectory_(trajectory), parameters_(parameters)
 {
     if (!trajectory || !robot_model || !parameters || !collision_space) {
@@ -73,6 +73,12 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
     d.stream = stream;
     d.rank = 0;
     d.world_size = 1;
+    d.inertias = robot_model->inertias.size() == robot_model->segments.size() ? robot_model->inertias.data() : nullptr;
+    d.torque_root = robot_model->torque_root;
+    d.torque_tip = robot_model->torque_tip;
+    for (int k = 0; k < 3; ++k) d.gravity[k] = robot_model->gravity[k];
+    d.num_orientation_constraints = (int32_t)constraints.orientation_constraints.size();
+    d.orientation_constraints = constraints.orientation_constraints.data();
     int rc = stomp_engine_create(&d, &engine_);
     if (rc) {
         error_ = engine_error(nullptr, rc);
@@ -157,10 +163,12 @@ bool StompOptimizer::executeBatch(const std::vector<std::vector<VectorXd>>& para
         }
     }
     std::vector<double> c((size_t)E * N_);
-    std::vector<uint8_t> cf(E > 0 ? E : 1);
+    std::vector<uint8_t> cf(E > 0 ? E : 1), cs(E > 0 ? E : 1);
     // StompOptimizer::iteration_ is iteration_number - 1 inside runSingleIteration
-    if (!check(stomp_engine_eval(engine_, prm.data(), E, c.data(), cf.data(), nullptr, iteration_number - 1)))
+    if (!check(stomp_engine_eval(engine_, prm.data(), E, c.data(), cf.data(), nullptr, iteration_number - 1,
+                                 cs.data())))
         return false;
+    if (E > 0) last_cs_ = cs[E - 1] != 0;
     costs.assign(E, VectorXd(N_));
     collision_free.assign(E, false);
     for (int r = 0; r < E; ++r) {
@@ -294,6 +302,7 @@ bool PolicyImprovementLoop::runSingleIteration(int iteration_number)
     }
     optimizer_->last_cost_ = out.cost;
     optimizer_->last_cf_ = out.collision_free != 0;
+    optimizer_->last_cs_ = out.constraints_satisfied != 0;
     return true;
 }
 

@@ -401,7 +401,8 @@ class Problem:
 
 def make_problem(dof: int = 7, waypoints: int = 100, grid_n: int = 64, num_rollouts: int = 10,
                  num_reused_rollouts: int = 5, build_grid: bool = True, seed: Optional[int] = None,
-                 with_pole: bool = True, start=None, goal=None, **param_overrides) -> Problem:
+                 with_pole: bool = True, start=None, goal=None, orientation_constraints=None,
+                 **param_overrides) -> Problem:
     robot = pr2like7() if dof == 7 else pr2like14()
     spheres = make_spheres(robot)
     max_exp = max(s.radius + s.clearance for s in spheres)
@@ -417,9 +418,18 @@ def make_problem(dof: int = 7, waypoints: int = 100, grid_n: int = 64, num_rollo
     p = Problem(robot, spheres, grid, boxes, cyls, params, np.array(start, np.float64), np.array(goal, np.float64))
     if seed is not None:
         p.seed = seed
+    if orientation_constraints:
+        p.orientation_constraints = list(orientation_constraints)
     if build_grid:
         p.sdf = build_sdf(grid, boxes, cyls)
     return p
+
+
+def upright_constraint(link: str = "r_gripper_tool_frame") -> OrientationConstraint:
+    """The reference's upright path constraint (test/test_omp.cpp:76-91): HEADER_FRAME, identity
+    nominal orientation, roll / pitch within 0.2 rad, yaw free (tolerance 10 >= pi), weight 1."""
+    return OrientationConstraint(link, (0.0, 0.0, 0.0, 1.0), header_frame=True, absolute_roll_tolerance=0.2,
+                                 absolute_pitch_tolerance=0.2, absolute_yaw_tolerance=10.0, weight=1.0)
 
 
 def _mirror(q):

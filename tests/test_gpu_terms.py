@@ -59,3 +59,64 @@ def test_torque_optimize_bitwise():
         (ost.iterations, ost.success_iteration, ost.last_improvement_iteration)
     np.testing.assert_array_equal(ecosts, ocosts)
     np.testing.assert_array_equal(e.best_trajectory(), o.best_trajectory())
+
+
+def _constraints():
+    q = np.array([0.1, -0.2, 0.3, 0.9])
+    q /= np.linalg.norm(q)
+    return [pb.upright_constraint(),
+            pb.OrientationConstraint("r_wrist_roll_link", tuple(q), header_frame=False, absolute_roll_tolerance=0.5,
+                                     absolute_pitch_tolerance=0.4, absolute_yaw_tolerance=0.3, weight=2.0)]
+
+
+@pytest.mark.parametrize("torque", [0.0, 0.001])
+def test_constraints_execute_bitwise(torque):
+    p = make(torque_cost_weight=torque, orientation_constraints=_constraints())
+    o, e = po.Oracle(p), eng.Engine(p)
+    rng = np.random.default_rng(8)
+    th = o.theta()
+    params = th[None] + rng.standard_normal((6, p.J, p.N)).cumsum(axis=2) * 0.05
+    params[0] = th
+    params[5] = 0.0   # every joint at zero: identity-like rotations (KDL quaternion trace branch edges)
+    params[3, 4] += np.pi   # forearm roll half a turn: the quaternion's single-precision branches
+    params[4, 6] += 2.5
+    costs, cf, traj = e.execute(params, iteration_member=1)
+    ecs = e.last_constraints_satisfied
+    for r in range(params.shape[0]):
+        oc, ocf, otr = o.execute(params[r], iteration_member=1)
+        np.testing.assert_array_equal(traj[r], otr)
+        np.testing.assert_array_equal(costs[r], oc)
+        assert bool(cf[r]) == ocf and bool(ecs[r]) == o.last_constraints_satisfied
+
+
+def test_constraints_iterations_and_optimize_bitwise():
+    p = make(K=20, Kr=10, orientation_constraints=_constraints()[:1], max_iterations=30,
+             max_iterations_after_collision_free=5)
+    o, e = po.Oracle(p), eng.Engine(p)
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+        assert e.last_constraints_satisfied == o.last_constraints_satisfied
+    o, e = po.Oracle(p), eng.Engine(p)
+    ost, ocosts = o.optimize()
+    est, ecosts = e.optimize()
+    assert (est.iterations, est.success, est.success_iteration, est.collision_success_iteration,
+            est.last_improvement_iteration) == (ost.iterations, ost.success, ost.success_iteration,
+                                                ost.collision_success_iteration, ost.last_improvement_iteration)
+    np.testing.assert_array_equal(ecosts, ocosts)
+    np.testing.assert_array_equal(e.best_trajectory(), o.best_trajectory())
+
+
+def test_golden_terms_cases():
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "terms_cases.npz"))
+    p = pb.make_problem(grid_n=64, num_rollouts=10, num_reused_rollouts=5, torque_cost_weight=0.001,
+                        orientation_constraints=[pb.upright_constraint()])
+    e = eng.Engine(p)
+    costs, cf, _ = e.execute(g["params"], iteration_member=1)
+    np.testing.assert_array_equal(costs, g["costs"])
+    np.testing.assert_array_equal(cf, g["cf"])
+    np.testing.assert_array_equal(e.last_constraints_satisfied, g["cs"])
+    for it in range(1, 6):
+        c, _ = e.iterate(it)
+        assert c == g["it_costs"][it - 1] and e.last_constraints_satisfied == g["it_cs"][it - 1]
+        np.testing.assert_array_equal(e.theta(), g["theta"][it - 1])

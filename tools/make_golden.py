@@ -101,6 +101,32 @@ def optimize_fixture():
                          st.last_improvement_iteration]), best_cost=np.array([st.best_cost]))
 
 
+def terms_fixture():
+    # torque term (launch/stomp_motion_planner_torques.launch:12 weight) + the upright path
+    # constraint of test/test_omp.cpp:76-91, params.yaml 10 / 5 rollouts
+    p = pb.make_problem(grid_n=64, num_rollouts=10, num_reused_rollouts=5, torque_cost_weight=0.001,
+                        orientation_constraints=[pb.upright_constraint()])
+    o = po.Oracle(p)
+    rng = np.random.default_rng(21)
+    th = o.theta()
+    params = np.stack([th + s * rng.standard_normal(th.shape) for s in (0.0, 0.05, 0.3)] + [th.copy()])
+    params[3, 4] += np.pi
+    costs, cfs, css = [], [], []
+    for prm in params:
+        c, cf, _ = o.execute(prm, 1)
+        costs.append(c)
+        cfs.append(cf)
+        css.append(o.last_constraints_satisfied)
+    it_costs, it_cs, thetas = [], [], []
+    for it in range(1, 6):
+        c, _ = o.iterate(it)
+        it_costs.append(c)
+        it_cs.append(o.last_constraints_satisfied)
+        thetas.append(o.theta())
+    save("terms_cases", params=params, costs=np.stack(costs), cf=np.array(cfs), cs=np.array(css),
+         it_costs=np.array(it_costs), it_cs=np.array(it_cs), theta=np.stack(thetas))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     math_kats()
@@ -108,3 +134,4 @@ if __name__ == "__main__":
     execute_fixture()
     iterate_fixture()
     optimize_fixture()
+    terms_fixture()
