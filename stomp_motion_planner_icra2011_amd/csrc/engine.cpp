@@ -55,6 +55,10 @@ struct stomp_engine {
     bool terms_on = false;      // torque term / path constraints: k_terms after every k_rollout
     double* d_terms_traj = nullptr;   // [K_loc][J][N] joint-limited trajectories for k_terms
     uint8_t* d_cs = nullptr;          // last_trajectory_constraints_satisfied_ of the noiseless rollout
+    DevTrack* d_track = nullptr;      // device-resident optimize loop state; d_track->stop gates every launch
+    const int* d_stop = nullptr;
+    double* d_opt_costs = nullptr;    // [max_iterations] last_trajectory_cost_ per iteration
+    DevTrack* h_track = nullptr;      // pinned read-back slots
     std::vector<FkOp> ops;
     std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
     int nslots = 0;
@@ -311,6 +315,7 @@ void release(stomp_engine* e)
     for (void* p : e->allocs) hipFree(p);
     if (e->h_total) hipHostFree(e->h_total);
     if (e->h_cf) hipHostFree(e->h_cf);
+    if (e->h_track) hipHostFree(e->h_track);
 #ifdef STOMP_WITH_RCCL
     if (e->comm) ncclCommDestroy(e->comm);
 #endif
@@ -324,6 +329,7 @@ void launch_terms_for(stomp_engine* e, const CostArgs& ca, uint8_t* cs = nullptr
     if (!e->terms_on) return;
     Timed tm(e, T_TERMS);
     TermsArgs ta{};
+    ta.stop = e->d_stop;
     ta.traj = ca.traj_out; ta.state = ca.state_out; ta.total = ca.total_out; ta.num_noisy = ca.num_noisy;
     ta.cs = cs;
     if (ca.x_params) {
@@ -336,6 +342,7 @@ void launch_terms_for(stomp_engine* e, const CostArgs& ca, uint8_t* cs = nullptr
 void launch_noiseless(stomp_engine* e, int member)
 {
     CostArgs ca{};
+    ca.stop = e->d_stop;
     ca.num_noisy = 0;
     ca.x_params = e->d_theta; ca.x_member = member;
     ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
@@ -378,6 +385,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     const double w = 0.5 * e->w_smooth;   // policy_improvement.cpp:487
     for (int r = 0; r < 3; ++r) na.wr[r] = w * e->smooth[r];
     na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0; na.row_begin = 0;
+    na.stop = e->d_stop;
     if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
 
     // generateRollouts bookkeeping (policy_improvement.cpp:167-175)
@@ -390,7 +398,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         Timed tm(e, T_REUSE);
         launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, e->extra_added ? 1 : 0, e->d_params, e->d_noise, e->d_state,
                      e->d_control, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params,
-                     e->d_tmp_state, e->stream);
+                     e->d_tmp_state, e->d_stop, e->stream);
         e->extra_added = false;
     }
     na.K_gen_global = e->K_gen;
@@ -411,6 +419,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     // Task::execute for the generated rollouts of this shard (+ the pending noiseless rollout)
     {
         CostArgs ca{};
+        ca.stop = e->d_stop;
         ca.fused_noise = fused ? 1 : 0;
         ca.nz = na;
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
@@ -428,6 +437,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         launch_terms_for(e, ca);
     }
     WeightArgs wa{};
+    wa.stop = e->d_stop;
     wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
     wa.state = e->d_state; wa.control = e->d_control; wa.noise = e->d_noise;
     wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
@@ -474,7 +484,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     {
         Timed tm(e, T_UPDATE);
         launch_update(e->J, e->N, e->d_MT, e->d_u, e->split_modes ? e->d_u_all : nullptr, e->K / kSumBlock,
-                      e->d_theta, e->stream);
+                      e->d_theta, e->d_stop, e->stream);
     }
     if (pipelined) {
         e->pending_member = member;
@@ -686,6 +696,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_total, 1));
     CREATE_TRY(dev_alloc(e, &e->d_cf, 1));
     CREATE_TRY(dev_alloc(e, &e->d_cs, 1));
+    CREATE_TRY(dev_alloc(e, &e->d_track, 1));
+    e->d_stop = &e->d_track->stop;
+    CREATE_TRY(dev_alloc(e, &e->d_opt_costs, (size_t)std::max(e->max_it, 1)));
+    if (hipHostMalloc((void**)&e->h_track, sizeof(DevTrack) * 4) != hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
+    if (hipMemsetAsync(e->d_track, 0, sizeof(DevTrack), e->stream) != hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     if (hipMemsetAsync(e->d_cs, 1, 1, e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
@@ -953,43 +970,81 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
     return 0;
 }
 
-// StompOptimizer::optimize loop (stomp_optimizer.cpp:284-359), one read-back per iteration
+// StompOptimizer::optimize loop (stomp_optimizer.cpp:284-359), device-resident: every iteration is
+// followed by k_track, which keeps the loop's bookkeeping in HBM and sets the stop flag when the
+// reference loop would break; all later launches of the loop then return at once.  The host
+// enqueues iterations in chunks, one chunk ahead of the stop flag it reads back, so the stream
+// never waits on the host.
 int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it)
 {
-    stomp_stats s;
-    s.collision_success_iteration = -1;
-    s.success_iteration = -1;
-    s.success = 0;
-    s.last_improvement_iteration = -1;
-    int cfi = 0, it;
-    double best = 0.0;
-    const size_t bytes = sizeof(double) * e->J * e->N;
-    for (it = 0; it < e->max_it; it++) {
-        stomp_iter_out o;
-        int rc = stomp_engine_iterate(e, it + 1, &o);
-        if (rc) return rc;
-        const bool ok = o.collision_free && o.constraints_satisfied;   // stomp_optimizer.cpp:301-339
-        if (ok) cfi++;
-        else cfi = 0;
-        if (o.collision_free && s.collision_success_iteration == -1) s.collision_success_iteration = it;
-        if (ok && s.success_iteration == -1) {
-            s.success_iteration = it;
-            s.success = 1;
+    flush_noiseless(e);
+    DevTrack init{};
+    init.stop = 0; init.cfi = 0; init.iterations = 0; init.success = 0;
+    init.success_iteration = -1; init.collision_success_iteration = -1; init.last_improvement_iteration = -1;
+    init.best = 0.0;
+    e->h_track[3] = init;
+    HIP_TRY(e, hipMemcpyAsync(e->d_track, &e->h_track[3], sizeof(DevTrack), hipMemcpyHostToDevice, e->stream));
+    const int max_it = e->max_it;
+    const int JN = e->J * e->N;
+    // host-side generateRollouts state after each iteration, to restore the one the device stopped at
+    struct HostState { bool reused_next, extra_added; };
+    std::vector<HostState> after((size_t)std::max(max_it, 1));
+    const int chunk = 8;
+    int next = 0, checked = 0;
+    hipEvent_t ev[2] = {get_event(e), get_event(e)};
+    int slot_end[2] = {0, 0};
+    int inflight = 0, head = 0;
+    auto enqueue_chunk = [&](int slot) -> int {
+        const int end = std::min(next + chunk, max_it);
+        for (; next < end; ++next) {
+            int rc = enqueue_iteration(e, next + 1, false);
+            if (rc) return rc;
+            launch_track(e->d_track, next, e->max_it_cf, e->d_total, e->d_cf, e->d_cs, e->d_opt_costs, e->d_last_traj,
+                         e->d_best_traj, JN, e->stream);
+            after[next] = {e->reused_next, e->extra_added};
         }
-        if (costs_per_it) costs_per_it[it] = o.cost;
-        if (it == 0 || (o.cost < best && ok)) {
-            HIP_TRY(e, hipMemcpyAsync(e->d_best_traj, e->d_last_traj, bytes, hipMemcpyDeviceToDevice, e->stream));
-            best = o.cost;
-            if (it != 0) s.last_improvement_iteration = it;
+        HIP_TRY(e, hipMemcpyAsync(&e->h_track[slot], e->d_track, sizeof(DevTrack), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipEventRecord(ev[slot], e->stream));
+        slot_end[slot] = next;
+        return 0;
+    };
+    int rc = 0;
+    bool stopped = false;
+    while (!stopped && checked < max_it) {
+        while (inflight < 2 && next < max_it) {
+            if ((rc = enqueue_chunk((head + inflight) & 1))) break;
+            ++inflight;
         }
-        if (cfi >= e->max_it_cf) {
-            it++;
-            break;
-        }
+        if (rc || inflight == 0) break;
+        HIP_TRY(e, hipEventSynchronize(ev[head]));
+        const DevTrack& h = e->h_track[head];
+        checked = slot_end[head];
+        stopped = h.stop != 0;
+        head ^= 1;
+        --inflight;
     }
-    s.iterations = it;
-    s.best_cost = best;
     HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->pool.push_back(ev[0]);
+    e->pool.push_back(ev[1]);
+    if (rc) return rc;
+    DevTrack& t = e->h_track[2];
+    HIP_TRY(e, hipMemcpy(&t, e->d_track, sizeof(DevTrack), hipMemcpyDeviceToHost));
+    if (t.iterations > 0) {
+        e->reused_next = after[t.iterations - 1].reused_next;
+        e->extra_added = after[t.iterations - 1].extra_added;
+    }
+    if (costs_per_it && t.iterations > 0)
+        HIP_TRY(e, hipMemcpy(costs_per_it, e->d_opt_costs, sizeof(double) * t.iterations, hipMemcpyDeviceToHost));
+    // later launches (iterate / run / eval) are not gated
+    HIP_TRY(e, hipMemsetAsync(e->d_track, 0, sizeof(int), e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    stomp_stats s;
+    s.iterations = t.iterations;
+    s.success = t.success;
+    s.success_iteration = t.success_iteration;
+    s.collision_success_iteration = t.collision_success_iteration;
+    s.last_improvement_iteration = t.last_improvement_iteration;
+    s.best_cost = t.best;
     if (st) *st = s;
     return 0;
 }

@@ -98,6 +98,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ int flag;
     __shared__ int nz_count;
+    if (a.stop && *a.stop) return;
     const int J = m.J, N = m.N, S = m.S;
     const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
     double* traj = (double*)(lds_raw + L.traj);   // J*N

@@ -48,8 +48,9 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
                                                double* noise, double* state, const double* control,
                                                const double* x_params, const double* x_state,
                                                const double* x_control, const double* theta, double* tmp_params,
-                                               double* tmp_state)
+                                               double* tmp_state, const int* stop)
 {
+    if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int n = K + with_extra;
     double* costs = sh;
@@ -112,11 +113,54 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
 void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,
                   double* state, const double* control, const double* x_params, const double* x_state,
                   const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
-                  hipStream_t s)
+                  const int* stop, hipStream_t s)
 {
     const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
     hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, params, noise, state,
-                       control, x_params, x_state, x_control, theta, tmp_params, tmp_state);
+                       control, x_params, x_state, x_control, theta, tmp_params, tmp_state, stop);
+}
+
+// StompOptimizer::optimize bookkeeping (stomp_optimizer.cpp:301-344) for iteration index `it`
+// (iteration_), after its noiseless rollout: collision-free streak, success / collision-success
+// iterations, the cost history, best_group_trajectory_ (copied by the whole block) and the
+// break condition, which turns every later launch of the loop into a no-op.
+__global__ __launch_bounds__(256) void k_track(DevTrack* tr, int it, int max_it_cf, const double* total,
+                                               const uint8_t* cf, const uint8_t* cs, double* costs,
+                                               const double* last_traj, double* best_traj, int JN)
+{
+    __shared__ int copy;
+    if (tr->stop) return;   // uniform: every thread reads the same flag before any write
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double cost = *total;
+        const bool cfree = *cf != 0;
+        const bool ok = cfree && *cs != 0;
+        tr->cfi = ok ? tr->cfi + 1 : 0;
+        if (cfree && tr->collision_success_iteration == -1) tr->collision_success_iteration = it;
+        if (ok && tr->success_iteration == -1) {
+            tr->success_iteration = it;
+            tr->success = 1;
+        }
+        costs[it] = cost;
+        copy = 0;
+        if (it == 0 || (cost < tr->best && ok)) {
+            tr->best = cost;
+            if (it != 0) tr->last_improvement_iteration = it;
+            copy = 1;
+        }
+        tr->iterations = it + 1;
+        if (tr->cfi >= max_it_cf) tr->stop = 1;
+    }
+    __syncthreads();
+    if (copy)
+        for (int i = threadIdx.x; i < JN; i += blockDim.x) best_traj[i] = last_traj[i];
+}
+
+void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, const uint8_t* cf, const uint8_t* cs,
+                  double* costs, const double* last_traj, double* best_traj, int JN, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_track, dim3(1), dim3(256), 0, s, tr, it, max_it_cf, total, cf, cs, costs, last_traj,
+                       best_traj, JN);
 }
 
 // ============================================================== distance field construction

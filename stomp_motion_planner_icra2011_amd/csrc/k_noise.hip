@@ -26,6 +26,7 @@ template <int BLOCK, int RT>
 __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    if (a.stop && *a.stop) return;
     const int N = a.N, Nall = a.Nall, J = a.J;
     const int NB = N + kBandBatch;   // rows incl. the zero padding the band products read
     double* zs = lds;              // NB*RT  [k][rr]

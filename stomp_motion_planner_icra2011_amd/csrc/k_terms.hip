@@ -162,6 +162,7 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    if (a.stop && *a.stop) return;
     const int J = m.J, N = m.N, nc = m.nchain;
     double* Q = (double*)lds_raw;            // [3][J][N]
     double* F = Q + (size_t)3 * J * N;       // [nc][6][N]

@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
     __shared__ double mn_s[16], den_s[16], ps_s[16];
+    if (a.stop && *a.stop) return;
     const int TC = a.tc, N = a.N, J = a.J, K = a.K_loc;
     const int tid = threadIdx.x, c = tid % TC;
     const int d = blockIdx.y, t0 = blockIdx.x * TC, t = t0 + c;
@@ -223,6 +224,7 @@ __global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
     __shared__ double mn_s[TCW], den_s[TCW], ps_s[TCW];
+    if (a.stop && *a.stop) return;
     const int N = a.N, J = a.J, K = a.K_loc;
     const int JN = J * N;
     const int tid = threadIdx.x, cc = tid % TCW, rs = tid / TCW;
@@ -445,7 +447,7 @@ void launch_weights(const WeightArgs& a, hipStream_t s)
 __global__ void k_cumulative(WeightArgs a, double* cum)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.K_loc * a.J) return;
+    if (idx >= a.K_loc * a.J || (a.stop && *a.stop)) return;
     const int r = idx / a.J, d = idx % a.J;
     const int N = a.N;
     double* c = cum + ((size_t)r * a.J + d) * N;
@@ -465,9 +467,10 @@ void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s)
 // delta = M u (policy_improvement.cpp:380), theta += 1.0 * delta (covariant_trajectory_policy.cpp:318-323).
 // With u_all (multi-GPU) u is first summed over the all-gathered block partials in block order.
 __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
-                                                int nb_total, double* theta)
+                                                int nb_total, double* theta, const int* stop)
 {
     __shared__ double us[256 + kBandBatch];
+    if (stop && *stop) return;
     const int d = blockIdx.x, i = threadIdx.x;
     if (i < kBandBatch) us[N + i] = 0.0;
     const size_t JN = (size_t)J * N;
@@ -492,9 +495,9 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
 }
 
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,
-                   hipStream_t s)
+                   const int* stop, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_update, dim3(J), dim3(256), 0, s, J, N, MT, u, u_all, nb_total, theta);
+    hipLaunchKernelGGL(k_update, dim3(J), dim3(256), 0, s, J, N, MT, u, u_all, nb_total, theta, stop);
 }
 
 }  // namespace stomp

@@ -136,12 +136,14 @@ struct NoiseArgs {
     double* noise;
     double* control;
     int zero_noise;             // extra rollout: params given, noise = 0 (addExtraRollouts)
+    const int* stop;            // device-resident optimize loop: nonzero -> the launch is a no-op
     int row_begin;              // only rows [row_begin, K_loc) (reused rows after the reuse kernel)
 };
 
 // Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
 // x_params) evaluates the noiseless rollout of theta (pipelined from the previous iteration).
 struct CostArgs {
+    const int* stop;            // nonzero -> no-op (device-resident optimize loop)
     int fused_noise;            // blocks < num_noisy first generate their row (NoiseArgs nz):
     NoiseArgs nz;               // normals, L z, params, M eps, control costs (k_noise's work)
     const double* params;
@@ -163,6 +165,7 @@ struct CostArgs {
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
 
 struct WeightArgs {
+    const int* stop;            // nonzero -> no-op
     int J, N, K_loc, use_cumulative, mode, tc, nb_total;
     const double* state;        // [K][N]
     const double* control;      // [K][J][N]
@@ -212,6 +215,7 @@ struct TermsModel {
 };
 
 struct TermsArgs {
+    const int* stop;            // nonzero -> no-op
     const double* traj;         // [num_noisy][J][N] joint-limited trajectories
     double* state;              // [num_noisy][N] in: w_obs * collision cost; out: the full costs
     double* total;              // [num_noisy] or null
@@ -227,6 +231,16 @@ size_t terms_lds_bytes(const TermsModel& m);
 void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
 
 void launch_noise(const NoiseArgs& a, hipStream_t s);
+
+// StompOptimizer::optimize bookkeeping on the device (stomp_optimizer.cpp:301-344), one launch
+// after each iteration's noiseless rollout; sets stop when the loop would break
+struct DevTrack {
+    int stop, cfi, iterations, success, success_iteration, collision_success_iteration, last_improvement_iteration;
+    int pad;
+    double best;
+};
+void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, const uint8_t* cf, const uint8_t* cs,
+                  double* costs, const double* last_traj, double* best_traj, int JN, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);
 size_t rollout_lds_bytes(const DevModel& m, int pad_lds);   // dynamic LDS of the rollout kernel
@@ -241,13 +255,13 @@ void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
 void launch_weights(const WeightArgs& a, hipStream_t s);
 int weights_tile(int K_loc);
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
-                   double* theta, hipStream_t s);
+                   double* theta, const int* stop, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);
 void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,
                   double* state, const double* control, const double* x_params, const double* x_state,
                   const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
-                  hipStream_t s);
+                  const int* stop, hipStream_t s);
 void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes /*n x 6 idx ranges*/,
                       int nb, const long long* cyl_d2 /*nc x nx x ny*/, const int* cyl_z /*nc x 2*/, int nc,
                       float* out, hipStream_t s);

@@ -225,3 +225,24 @@ def test_golden_execute_cases():
         np.testing.assert_array_equal(c, g[f"costs_{dof}"])
         np.testing.assert_array_equal(tr, g[f"traj_{dof}"])
         np.testing.assert_array_equal(cf, g[f"cf_{dof}"])
+
+
+@pytest.mark.parametrize("K,Kr,after_cf", [(20, 10, 3), (10, 0, 1), (20, 10, 1000)])
+def test_device_optimize_loop_stops_like_the_reference(K, Kr, after_cf):
+    # the device-resident loop (k_track + stop flag, chunks enqueued ahead) must stop at the
+    # reference's iteration (stomp_optimizer.cpp:340-344), leave theta as the last executed
+    # iteration did, and let plain iterations continue from there
+    p = make(K=K, Kr=Kr, max_iterations=37, max_iterations_after_collision_free=after_cf)
+    o, e = po.Oracle(p), eng.Engine(p)
+    ost, ocosts = o.optimize()
+    est, ecosts = e.optimize()
+    assert (est.iterations, est.success, est.success_iteration, est.collision_success_iteration,
+            est.last_improvement_iteration) == (ost.iterations, ost.success, ost.success_iteration,
+                                                ost.collision_success_iteration, ost.last_improvement_iteration)
+    assert est.best_cost == ost.best_cost
+    np.testing.assert_array_equal(ecosts, ocosts)
+    np.testing.assert_array_equal(e.best_trajectory(), o.best_trajectory())
+    np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory())
+    np.testing.assert_array_equal(e.theta(), o.theta())
+    for it in range(est.iterations + 1, est.iterations + 3):
+        _compare_iteration(o, e, it)
