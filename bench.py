@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event pass (no roofline)")
+    ap.add_argument("--problems", type=int, default=1,
+                    help="independent planning problems per GPU, one engine and stream each (cfg5 mode)")
+    ap.add_argument("--optimize-steps", type=int, default=200,
+                    help="also time StompOptimizer::optimize (device-resident loop) for this many iterations (0 = skip)")
     return ap.parse_args()
 
 
@@ -79,6 +83,63 @@ def cpu_baseline(problem, budget_s: float):
                       f"(dense N x N products, sequential Task::execute), 1 thread, {el:.1f} s"}
 
 
+def bench_problems(args, world, rank, local_rank, dist):
+    """cfg5: independent planning problems per GPU (distinct start / goal / seed, one shared
+    device-built SDF), one engine and one stream each, no communication (replicas); the steps
+    are enqueued round-robin over the engines so the streams run concurrently.  value =
+    problem-iterations per second over all ranks."""
+    from stomp_motion_planner_icra2011_amd import engine as eng
+    from stomp_motion_planner_icra2011_amd import problem as pb
+    P = args.problems
+    rng = np.random.default_rng(1234 + rank)
+    base = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=args.rollouts_per_gpu,
+                           num_reused_rollouts=0, build_grid=False)
+    sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
+    eng.sdf_build_device(base, sdf.ptr)
+    engines = []
+    for i in range(P):
+        d = rng.uniform(-0.15, 0.15, (2, base.J))
+        p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid,
+                            num_rollouts=args.rollouts_per_gpu, num_reused_rollouts=0, build_grid=False,
+                            seed=base.seed + 1 + rank * P + i, start=list(base.start + d[0]), goal=list(base.goal + d[1]),
+                            max_iterations=args.warmup + args.steps + 1)
+        engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr))
+
+    def sweep(first, count):
+        for k in range(count):
+            for e in engines:
+                e.run(first + k, 1)
+        for e in engines:
+            e.synchronize()
+
+    sweep(1, args.warmup)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    sweep(args.warmup + 1, args.steps)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = P * world * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "STOMP problem-iterations/sec (64-problem batch, cfg5)", "value": round(value, 3),
+            "unit": "problem-iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (PR2-like arm, shelf+pole scene, device-built SDF; Philox noise)",
+            "config": {"workload": f"cfg5: {P} problems/GPU x {world} GPU, {args.dof}-DOF, {args.waypoints} wp, "
+                                   f"K={args.rollouts_per_gpu} each, {args.grid}^3 SDF shared",
+                       "problems_per_gpu": P, "parallelism": f"replicas x{world}, one stream per problem",
+                       "rollouts_per_s": round(value * args.rollouts_per_gpu, 1)}}))
+    for e in engines:
+        e.close()
+    sdf.free()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,6 +154,12 @@ def main():
 
     from stomp_motion_planner_icra2011_amd import engine as eng
     from stomp_motion_planner_icra2011_amd import problem as pb
+
+    if args.problems > 1:
+        bench_problems(args, world, rank, local_rank, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     K = args.rollouts_per_gpu * world
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
@@ -160,6 +227,23 @@ def main():
         roofline["iteration_bytes"] = b_iter
         roofline["iteration_frac"] = round(b_iter * value / (HBM_PEAK_GBS * 1e9 * world), 5)   # vs N x peak
 
+    # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
+    # the same iterations with the optimizer's bookkeeping, no early stop
+    optimize = None
+    if args.optimize_steps > 0:
+        po_ = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
+                              num_reused_rollouts=0, build_grid=False, max_iterations=args.optimize_steps,
+                              max_iterations_after_collision_free=args.optimize_steps + 1)
+        eo = eng.Engine(po_, device=local_rank, sdf_device_ptr=sdf.ptr, rank=rank, world_size=world, comm_id=comm_id) \
+            if world == 1 else None
+        if eo is not None:
+            eo.optimize()   # warm
+            t0 = time.perf_counter()
+            st, _ = eo.optimize()
+            dt = time.perf_counter() - t0
+            optimize = {"iterations": st.iterations, "iterations_per_s": round(st.iterations / dt, 3)}
+            eo.close()
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         pc = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
@@ -180,6 +264,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_timing_us": {k: round(v["avg_us"], 3) for k, v in timing.items()},
+            "optimize_loop": optimize,
         }
         print(json.dumps(out))
     e.close()
