@@ -59,6 +59,7 @@ struct stomp_engine {
     const int* d_stop = nullptr;
     double* d_opt_costs = nullptr;    // [max_iterations] last_trajectory_cost_ per iteration
     DevTrack* h_track = nullptr;      // pinned read-back slots
+    bool tracking = false;            // inside stomp_engine_optimize: k_track after each noiseless rollout
     std::vector<FkOp> ops;
     std::vector<int> sphere_slot;   // published frame slot of each sphere's segment
     int nslots = 0;
@@ -338,6 +339,15 @@ void launch_terms_for(stomp_engine* e, const CostArgs& ca, uint8_t* cs = nullptr
     launch_terms(e->terms, ta, e->stream);
 }
 
+// the optimize loop's bookkeeping for the noiseless rollout a launch with these arguments
+// evaluated (its iteration_ is ca.x_member)
+void track_noiseless(stomp_engine* e, const CostArgs& ca)
+{
+    if (!e->tracking || !ca.x_params) return;
+    launch_track(e->d_track, ca.x_member, e->max_it_cf, e->d_total, e->d_cf, e->d_cs, e->d_opt_costs, e->d_last_traj,
+                 e->d_best_traj, e->J * e->N, e->stream);
+}
+
 // noiseless rollout of the current theta (policy_improvement_loop.cpp:180-182), alone
 void launch_noiseless(stomp_engine* e, int member)
 {
@@ -351,6 +361,7 @@ void launch_noiseless(stomp_engine* e, int member)
         launch_cost(e->model, ca, e->stream);
     }
     launch_terms_for(e, ca);
+    track_noiseless(e, ca);
 }
 
 int flush_noiseless(stomp_engine* e)
@@ -435,6 +446,9 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             launch_cost(e->model, ca, e->stream);
         }
         launch_terms_for(e, ca);
+        // before this iteration's weights / update: a break decided on the previous
+        // iteration's noiseless rollout leaves theta where the reference leaves it
+        track_noiseless(e, ca);
     }
     WeightArgs wa{};
     wa.stop = e->d_stop;
@@ -985,7 +999,6 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     e->h_track[3] = init;
     HIP_TRY(e, hipMemcpyAsync(e->d_track, &e->h_track[3], sizeof(DevTrack), hipMemcpyHostToDevice, e->stream));
     const int max_it = e->max_it;
-    const int JN = e->J * e->N;
     // host-side generateRollouts state after each iteration, to restore the one the device stopped at
     struct HostState { bool reused_next, extra_added; };
     std::vector<HostState> after((size_t)std::max(max_it, 1));
@@ -997,10 +1010,10 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     auto enqueue_chunk = [&](int slot) -> int {
         const int end = std::min(next + chunk, max_it);
         for (; next < end; ++next) {
-            int rc = enqueue_iteration(e, next + 1, false);
+            // K_r = 0: the noiseless rollout of iteration next rides in the next iteration's
+            // rollout launch (pipelined), its k_track right after that launch
+            int rc = enqueue_iteration(e, next + 1, e->Kr == 0);
             if (rc) return rc;
-            launch_track(e->d_track, next, e->max_it_cf, e->d_total, e->d_cf, e->d_cs, e->d_opt_costs, e->d_last_traj,
-                         e->d_best_traj, JN, e->stream);
             after[next] = {e->reused_next, e->extra_added};
         }
         HIP_TRY(e, hipMemcpyAsync(&e->h_track[slot], e->d_track, sizeof(DevTrack), hipMemcpyDeviceToHost, e->stream));
@@ -1010,6 +1023,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     };
     int rc = 0;
     bool stopped = false;
+    e->tracking = true;
     while (!stopped && checked < max_it) {
         while (inflight < 2 && next < max_it) {
             if ((rc = enqueue_chunk((head + inflight) & 1))) break;
@@ -1023,6 +1037,8 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
         head ^= 1;
         --inflight;
     }
+    if (!rc) rc = flush_noiseless(e);   // the last iteration's noiseless rollout and its bookkeeping
+    e->tracking = false;
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->pool.push_back(ev[0]);
     e->pool.push_back(ev[1]);
