@@ -28,11 +28,14 @@ namespace stomp {
 namespace {
 constexpr int kMaxOps = 64;
 constexpr int kMaxSeg = 64;
-constexpr int kBlock = 256;
-#ifndef ROLLOUT_MIN_WAVES
-#define ROLLOUT_MIN_WAVES 3
+#ifndef ROLLOUT_BLOCK
+#define ROLLOUT_BLOCK 256
 #endif
-constexpr int kCopyBatch = 12;             // table-image words per lane per copy pass
+constexpr int kBlock = ROLLOUT_BLOCK;
+#ifndef ROLLOUT_MIN_WAVES
+#define ROLLOUT_MIN_WAVES (ROLLOUT_BLOCK > 256 ? 4 : 3)
+#endif
+constexpr int kCopyBatch = 12 * 256 / kBlock;   // table-image words per lane per copy pass
 #ifndef SPHERE_UNROLL
 #define SPHERE_UNROLL 2
 #endif

@@ -1,11 +1,12 @@
-# GPU tests, then bench A/B of an env switch (default vs "$1"=1); outputs under gpurun_out/ab
+# A/B of library variants at given rollout counts: args "variant:K" (variant "base" = product library)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
-timeout -k 10 500 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/ab/tests.log 2>&1 || { tail -40 gpurun_out/ab/tests.log; exit 1; }
-tail -2 gpurun_out/ab/tests.log
-for v in 0 1; do
-  env $1=$v timeout -k 10 200 python3 bench.py --cpu-seconds 0 > gpurun_out/ab/b$v.json 2> gpurun_out/ab/b$v.err || { tail -20 gpurun_out/ab/b$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/ab/b$v.json')); print('$1=$v', d['value'], d['kernel_timing_us'], d['optimize_loop'])"
+for vk in "$@"; do
+  v=${vk%%:*}; k=${vk##*:}
+  lib=$PWD/stomp_motion_planner_icra2011_amd/libstomp_engine_$v.so
+  [ "$v" = "base" ] && lib=$PWD/stomp_motion_planner_icra2011_amd/libstomp_engine.so
+  STOMP_ENGINE_LIB=$lib timeout -k 10 200 python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 --rollouts-per-gpu $k --optimize-steps 0 > gpurun_out/ab/$v.$k.json 2> gpurun_out/ab/$v.$k.err || { tail -5 gpurun_out/ab/$v.$k.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/$v.$k.json')); print('$v K=$k', d['value'], d['kernel_timing_us'])"
 done
