@@ -202,7 +202,7 @@ def main():
         e.set_timing(True)
         e.run(args.warmup + args.steps + 1, args.steps)
         e.synchronize()
-        for name in ("noise", "rollout_cost", "weights", "update", "noiseless", "all"):
+        for name in ("noise", "pregen", "rollout_cost", "weights", "update", "noiseless", "all"):
             tot, n = e.timing(name)
             timing[name] = {"total_ms": tot, "launches": n, "avg_us": 1000.0 * tot / max(n, 1)}
         e.set_timing(False)

@@ -31,8 +31,9 @@ namespace {
 
 thread_local std::string g_last_error;
 
-enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_TERMS, T_COUNT };
-const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse", "state_terms"};
+enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_TERMS, T_PREGEN, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse", "state_terms",
+                                    "pregen"};
 
 }  // namespace
 
@@ -79,6 +80,12 @@ struct stomp_engine {
     int pending_member = -1;   // iteration_ of a noiseless rollout of theta not evaluated yet
     double *d_mm = nullptr, *d_psum_part = nullptr, *d_psum_all = nullptr, *d_u_part = nullptr, *d_u_all = nullptr;
     int K_gen = 0;
+    // pregen (K_r = 0, fused noise phase): the normals, eps = sigma L z and M eps of iteration
+    // it + 1 are made by extra blocks of iteration it's weights launch (on CUs the weights tiles
+    // leave idle); the rollout launch of it + 1 reads them
+    bool pre_on = false;
+    int pre_it = -1;                  // iteration whose rows are in d_pre_eps / d_pre_meps (enqueued)
+    double *d_pre_eps = nullptr, *d_pre_meps = nullptr;
     double* h_total = nullptr;
     uint8_t* h_cf = nullptr;
     // eval scratch
@@ -159,19 +166,20 @@ hipEvent_t get_event(stomp_engine* e)
 struct Timed {
     stomp_engine* e;
     int id;
+    hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
-    Timed(stomp_engine* e_, int id_) : e(e_), id(id_)
+    Timed(stomp_engine* e_, int id_, hipStream_t s_ = nullptr) : e(e_), id(id_), s(s_ ? s_ : e_->stream)
     {
         if (e->timing) {
             a = get_event(e);
             b = get_event(e);
-            hipEventRecord(a, e->stream);
+            hipEventRecord(a, s);
         }
     }
     ~Timed()
     {
         if (e->timing) {
-            hipEventRecord(b, e->stream);
+            hipEventRecord(b, s);
             e->evs.push_back({id, a, b});
         }
     }
@@ -381,12 +389,10 @@ int flush_noiseless(stomp_engine* e)
     } while (0)
 #endif
 
-// One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
-// pipelined: the noiseless rollout of the updated theta is not launched here but evaluated by
-// the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
-int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
+// generateRollouts' sampling arguments of iteration it (policy_improvement_loop.cpp:155-160:
+// sigma_d * decay_d^(it - 1))
+NoiseArgs noise_args(const stomp_engine* e, int it)
 {
-    const int member = it - 1;
     NoiseArgs na{};
     na.J = e->J; na.N = e->N; na.Nall = e->Nall; na.K_loc = e->K_loc; na.first_global = e->first;
     na.iteration = it; na.seed = e->seed;
@@ -397,6 +403,26 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     for (int r = 0; r < 3; ++r) na.wr[r] = w * e->smooth[r];
     na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0; na.row_begin = 0;
     na.stop = e->d_stop;
+    na.pre_eps = e->d_pre_eps; na.pre_meps = e->d_pre_meps;
+    return na;
+}
+
+// k_pregen's arguments for iteration it: no stop flag, so the rows stay valid for pre_it
+// whatever the optimize loop decides
+NoiseArgs pregen_args(const stomp_engine* e, int it)
+{
+    NoiseArgs na = noise_args(e, it);
+    na.stop = nullptr;
+    return na;
+}
+
+// One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
+// pipelined: the noiseless rollout of the updated theta is not launched here but evaluated by
+// the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
+int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
+{
+    const int member = it - 1;
+    NoiseArgs na = noise_args(e, it);
     if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
 
     // generateRollouts bookkeeping (policy_improvement.cpp:167-175)
@@ -423,6 +449,15 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     const bool fused = false;
 #endif
     if (fused) na.row_begin = num_gen;
+    // every local row generated (K_r = 0): eps and M eps come from k_pregen
+    const bool pre = fused && e->pre_on && num_gen == e->K_loc;
+    if (pre) {
+        if (e->pre_it != it) {   // not made ahead by the previous iteration's weights launch
+            Timed tm(e, T_PREGEN);
+            launch_pregen(pregen_args(e, it), e->K_loc, e->stream);
+        }
+        e->pre_it = -1;
+    }
     if (na.row_begin < na.K_loc) {
         Timed tm(e, T_NOISE);
         launch_noise(na, e->stream);
@@ -431,7 +466,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     {
         CostArgs ca{};
         ca.stop = e->d_stop;
-        ca.fused_noise = fused ? 1 : 0;
+        ca.fused_noise = pre ? 2 : (fused ? 1 : 0);
         ca.nz = na;
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
@@ -458,19 +493,27 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     wa.tc = weights_tile(e->K_loc);
     wa.nb_total = e->K / kSumBlock;
     wa.mm = e->d_mm; wa.psum_part = e->d_psum_part; wa.psum_all = e->d_psum_all; wa.u_part = e->d_u_part;
+    // the first weights launch carries the next iteration's pregen rows
+    NoiseArgs next{};
+    const NoiseArgs* carry = nullptr;
+    if (pre) {
+        next = pregen_args(e, it + 1);
+        carry = &next;
+        e->pre_it = it + 1;
+    }
     {
         Timed tm(e, T_WEIGHTS);
         if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
         if (!e->split_modes) {
             wa.mode = W_FUSED;
-            launch_weights(wa, e->stream);
+            launch_weights(wa, e->stream, carry);
         } else {
             // the sharded decomposition; with one rank (debug hook) the all-reduce is the
             // identity and the all-gathers are device copies
             const size_t JN = (size_t)e->J * e->N;
             const size_t nb_loc = (size_t)e->K_loc / kSumBlock;
             wa.mode = W_MINMAX;
-            launch_weights(wa, e->stream);
+            launch_weights(wa, e->stream, carry);
 #ifdef STOMP_WITH_RCCL
             if (e->world > 1)
                 NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
@@ -700,6 +743,17 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(dev_alloc(e, &e->d_psum_all, nb_tot * J * N));
         CREATE_TRY(dev_alloc(e, &e->d_u_part, nb_loc * J * N));
         CREATE_TRY(dev_alloc(e, &e->d_u_all, nb_tot * J * N));
+    }
+    {
+        // STOMP_PREGEN=0: the rollout kernel draws its own noise (A/B hook)
+        const char* pg = std::getenv("STOMP_PREGEN");
+#ifndef STOMP_SEPARATE_NOISE
+        e->pre_on = e->Kr == 0 && J <= 16 && weights_carry_pregen(e->K_loc) && !(pg && pg[0] == '0');
+#endif
+    }
+    if (e->pre_on) {
+        CREATE_TRY(dev_alloc(e, &e->d_pre_eps, KJN));
+        CREATE_TRY(dev_alloc(e, &e->d_pre_meps, KJN));
     }
     CREATE_TRY(dev_alloc(e, &e->d_x_params, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_noise, (size_t)J * N));

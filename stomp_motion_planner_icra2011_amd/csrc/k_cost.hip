@@ -128,14 +128,15 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     // drawn (or the trajectory is loaded); they are stored to LDS after that
     double* zA = (double*)(lds_raw + L.nzA);
     double* zB = (double*)(lds_raw + L.nzB);
-    const bool gen = a.fused_noise && !extra;
+    const bool gen = a.fused_noise == 1 && !extra;
+    const bool pre = a.fused_noise == 2 && !extra;
     unsigned long long img[kCopyBatch];
     const int nw = m.img_words;
 #pragma unroll
     for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
     if (gen) {
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
-    } else {
+    } else if (!pre) {
         const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
         for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
             double v[4];
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     }
     STAMP(6);
     if (gen) rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
+    else if (pre) rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid);
     if (tid == 0) flag = 0;
     __syncthreads();
     STAMP(1);
@@ -421,6 +423,31 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 }
 
 STOMP_STAMP_ACCESSORS(cost)
+
+// generateRollouts' normals and eps = sigma L z, computeProjectedNoise's M eps for one row per
+// workgroup (policy_improvement.cpp:228-236, 473-482): the theta-independent half of the
+// rollout kernel's noise phase, run on a side stream while the previous iteration's weights
+// and update occupy the main one
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_pregen(NoiseArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_pg[];
+    if (a.stop && *a.stop) return;
+    const RolloutLds L = rollout_lds(a.J, a.N, 0, 0, 0, 0, 0, 0, 0);
+    double* zA = (double*)lds_pg;
+    double* zB = (double*)(lds_pg + (L.nzB - L.nzA));
+    rollout_normals<BLOCK>(a, blockIdx.x, zA, zB, threadIdx.x);
+    if (a.J <= 8) rollout_pregen_ng<BLOCK, 2>(a, blockIdx.x, zA, zB, threadIdx.x);
+    else rollout_pregen_ng<BLOCK, 4>(a, blockIdx.x, zA, zB, threadIdx.x);
+}
+
+void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s)
+{
+    if (rows <= 0) return;
+    const RolloutLds L = rollout_lds(a.J, a.N, 0, 0, 0, 0, 0, 0, 0);
+    const size_t lds = 2 * (L.nzB - L.nzA);
+    hipLaunchKernelGGL((k_pregen<256>), dim3(rows), dim3(256), lds, s, a);
+}
 
 bool cost_supported(const DevModel& m)
 {

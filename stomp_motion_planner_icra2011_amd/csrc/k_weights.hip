@@ -216,11 +216,11 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
 // TCW = 16) and a wave's load covers 64 / TCW rows of it; lane (rs, cc) holds rows
 // rs, rs + RS, ... of column cc in registers.  Same phases, modes and canonical sums as
 // k_weights.
+// the body of k_weights_rows for tile block bid of nt; V = [K_loc][TCW] dynamic LDS
 template <int TCW, int EPT>
-__global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
+__device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int nt, double* V)
 {
     constexpr int BLOCK = 256, RS = BLOCK / TCW;
-    extern __shared__ __attribute__((aligned(16))) double V[];   // [K_loc][TCW]
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
     __shared__ double mn_s[TCW], den_s[TCW], ps_s[TCW];
@@ -231,8 +231,8 @@ __global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
     // XCD-grouped tiles: workgroups are dealt round-robin over the 8 XCDs, so block b takes
     // tile (b mod 8)-th group's (b / 8)-th tile and the tiles sharing a 128-B line of a row
     // meet in one XCD's L2 instead of each fetching the line from memory
-    const int nt = gridDim.x, x = blockIdx.x & 7, q8 = nt >> 3, r8 = nt & 7;
-    const int tile = x * q8 + min(x, r8) + (blockIdx.x >> 3);
+    const int x = bid & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int tile = x * q8 + min(x, r8) + (bid >> 3);
     const int c0 = tile * TCW, c = c0 + cc;
     const bool colok = c < JN;
     const int cl = min(c, JN - 1);
@@ -390,6 +390,35 @@ __global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
     STAMP(5);
 }
 
+template <int TCW, int EPT>
+__global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double V[];   // [K_loc][TCW]
+    weights_rows<TCW, EPT>(a, blockIdx.x, gridDim.x, V);
+}
+
+// The same launch also carries k_pregen's rows for the next iteration (blocks nw on): the
+// weights tiles occupy under 256 workgroups, so the theta-independent noise of iteration
+// it + 1 (normals, sigma L z, M eps; noise_device.h) fills the idle CUs in the same dispatch
+// instead of waiting for the next rollout launch.  Those blocks ignore the stop flag (their
+// rows stay valid whatever the optimize loop decides).
+template <int TCW, int EPT>
+__global__ __launch_bounds__(256) void k_weights_rows_pre(WeightArgs a, NoiseArgs na, int nw)
+{
+    extern __shared__ __attribute__((aligned(16))) double V[];
+    if ((int)blockIdx.x < nw) {
+        weights_rows<TCW, EPT>(a, blockIdx.x, nw, V);
+        return;
+    }
+    const RolloutLds L = rollout_lds(na.J, na.N, 0, 0, 0, 0, 0, 0, 0);
+    double* zA = V;
+    double* zB = (double*)((unsigned char*)V + (L.nzB - L.nzA));
+    const int r = blockIdx.x - nw;
+    rollout_normals<256>(na, r, zA, zB, threadIdx.x);
+    if (na.J <= 8) rollout_pregen_ng<256, 2>(na, r, zA, zB, threadIdx.x);
+    else rollout_pregen_ng<256, 4>(na, r, zA, zB, threadIdx.x);
+}
+
 STOMP_STAMP_ACCESSORS(weights)
 
 // columns per workgroup: as many as keep K_loc * TC <= 2048 (more workgroups, shorter
@@ -408,33 +437,59 @@ int weights_tile(int K_loc)
 #define WEIGHTS_ROWS_TCW 4
 #endif
 template <int EPT>
-static void launch_rows(const WeightArgs& a, hipStream_t s)
+static void launch_rows(const WeightArgs& a, const NoiseArgs* pre, hipStream_t s)
 {
     constexpr int TCW = WEIGHTS_ROWS_TCW;
     const int JN = a.J * a.N;
-    const size_t lds = (size_t)a.K_loc * TCW * sizeof(double);
+    const int nw = (JN + TCW - 1) / TCW;
+    size_t lds = (size_t)a.K_loc * TCW * sizeof(double);
+    if (pre) {
+        const RolloutLds L = rollout_lds(pre->J, pre->N, 0, 0, 0, 0, 0, 0, 0);
+        const size_t lp = 2 * (size_t)(L.nzB - L.nzA);
+        if (lp > lds) lds = lp;
+        static size_t raised_pre = 0;
+        if (lds > 48 * 1024 && lds > raised_pre) {
+            (void)hipFuncSetAttribute((const void*)k_weights_rows_pre<TCW, EPT>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            raised_pre = lds;
+        }
+        hipLaunchKernelGGL((k_weights_rows_pre<TCW, EPT>), dim3(nw + pre->K_loc), dim3(256), lds, s, a, *pre, nw);
+        return;
+    }
     static size_t raised = 0;   // opt in to more than the default 64 KB once per size
     if (lds > 48 * 1024 && lds > raised) {
         (void)hipFuncSetAttribute((const void*)k_weights_rows<TCW, EPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         raised = lds;
     }
-    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3((JN + TCW - 1) / TCW), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(256), lds, s, a);
 }
 
-void launch_weights(const WeightArgs& a, hipStream_t s)
+bool weights_carry_pregen(int K_loc)
+{
+#ifndef WEIGHTS_COLUMN_TILES
+    constexpr int RS = 256 / WEIGHTS_ROWS_TCW;
+    const int nb = (K_loc + kSumBlock - 1) / kSumBlock;
+    return nb * WEIGHTS_ROWS_TCW <= 256 && K_loc <= 32 * RS;
+#else
+    return false;
+#endif
+}
+
+void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre)
 {
 #ifndef WEIGHTS_COLUMN_TILES
     // row-coalesced flat-column tiles while a lane's rows fit its registers
     constexpr int RS = 256 / WEIGHTS_ROWS_TCW;
     const int nb = (a.K_loc + kSumBlock - 1) / kSumBlock;
     if (nb * WEIGHTS_ROWS_TCW <= 256) {
-        if (a.K_loc <= 4 * RS) return launch_rows<4>(a, s);
-        if (a.K_loc <= 8 * RS) return launch_rows<8>(a, s);
-        if (a.K_loc <= 16 * RS) return launch_rows<16>(a, s);
-        if (a.K_loc <= 32 * RS) return launch_rows<32>(a, s);
+        if (a.K_loc <= 4 * RS) return launch_rows<4>(a, pre, s);
+        if (a.K_loc <= 8 * RS) return launch_rows<8>(a, pre, s);
+        if (a.K_loc <= 16 * RS) return launch_rows<16>(a, pre, s);
+        if (a.K_loc <= 32 * RS) return launch_rows<32>(a, pre, s);
     }
 #endif
+    if (pre) launch_pregen(*pre, pre->K_loc, s);   // not reached: the engine checks weights_carry_pregen
     dim3 grid((a.N + a.tc - 1) / a.tc, a.J);
     const size_t lds = (size_t)a.K_loc * a.tc * sizeof(double);
     if ((size_t)a.K_loc * a.tc <= 2048 && WEIGHTS_TILE_ELEMS <= 2048)

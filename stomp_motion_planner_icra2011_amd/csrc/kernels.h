@@ -138,14 +138,17 @@ struct NoiseArgs {
     int zero_noise;             // extra rollout: params given, noise = 0 (addExtraRollouts)
     const int* stop;            // device-resident optimize loop: nonzero -> the launch is a no-op
     int row_begin;              // only rows [row_begin, K_loc) (reused rows after the reuse kernel)
+    double* pre_eps;            // [K_loc][J][N] eps = sigma L z made ahead of the rollout launch (k_pregen)
+    double* pre_meps;           // [K_loc][J][N] M eps, likewise
 };
 
 // Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
 // x_params) evaluates the noiseless rollout of theta (pipelined from the previous iteration).
 struct CostArgs {
     const int* stop;            // nonzero -> no-op (device-resident optimize loop)
-    int fused_noise;            // blocks < num_noisy first generate their row (NoiseArgs nz):
-    NoiseArgs nz;               // normals, L z, params, M eps, control costs (k_noise's work)
+    int fused_noise;            // blocks < num_noisy first generate their row (NoiseArgs nz): 1 = normals,
+    NoiseArgs nz;               // L z, params, M eps, control costs (k_noise's work); 2 = eps and M eps
+                                // from nz.pre_eps / pre_meps (k_pregen), then params and control costs
     const double* params;
     long long stride;
     int num_noisy;
@@ -231,6 +234,9 @@ size_t terms_lds_bytes(const TermsModel& m);
 void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
 
 void launch_noise(const NoiseArgs& a, hipStream_t s);
+// the theta-independent part of generateRollouts + computeProjectedNoise for rows [0, rows):
+// normals, eps = sigma L z and M eps into a.pre_eps / a.pre_meps (run ahead on a side stream)
+void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s);
 
 // StompOptimizer::optimize bookkeeping on the device (stomp_optimizer.cpp:301-344), one launch
 // after each iteration's noiseless rollout; sets stop when the loop would break
@@ -252,7 +258,9 @@ int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS a
 constexpr size_t kLdsPerCu = 144 * 1024;
 constexpr size_t kRolloutLdsMax = 156 * 1024;                // dynamic + static per workgroup
 void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
-void launch_weights(const WeightArgs& a, hipStream_t s);
+// pre: also make the next iteration's k_pregen rows in the same launch (weights_carry_pregen)
+void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre = nullptr);
+bool weights_carry_pregen(int K_loc);
 int weights_tile(int K_loc);
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
                    double* theta, const int* stop, hipStream_t s);

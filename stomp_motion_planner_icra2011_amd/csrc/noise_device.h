@@ -255,6 +255,9 @@ __device__ __forceinline__ void mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, in
     if (rem >= 3) run(R2, bi + 2);
 }
 
+template <int BLOCK>
+__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid);
+
 template <int BLOCK, int NG>
 __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                    int tid)
@@ -318,6 +321,16 @@ __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, do
             if (i < N && d < J) xs[d * Nall + i + 6] = traj[d * N + i] + acc[g];
         }
     }
+    rollout_control<BLOCK>(a, row, xs, zB, tid);   // eps is dead
+}
+
+// computeControlCosts of one row from xs = the free part of params + M eps at [d][6 + i]
+// (written by the caller, not yet synchronised): the padding, the 7-tap terms into cs and the
+// control row to HBM
+template <int BLOCK>
+__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid)
+{
+    const int J = a.J, N = a.N, Nall = a.Nall;
     for (int idx = tid; idx < J * 12; idx += BLOCK) {
         const int d = idx / 12, k = idx - d * 12;
         xs[d * Nall + (k < 6 ? k : N + k)] = k < 6 ? a.start[d] : a.goal[d];
@@ -325,7 +338,6 @@ __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, do
     __syncthreads();
 
     STAMP(9);
-    double* cs = zB;   // eps is dead
     {
         // lane = (joint, run of kCtlRun consecutive padded indices): one 7-tap window read
         // serves the run; taps outside [0, Nall) are skipped as in control_term
@@ -369,6 +381,89 @@ __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, do
         }
     }
     STAMP(63);
+}
+
+// k_pregen's row: normals (rollout_normals, already issued), eps = sigma_d (0 + L z) and M eps,
+// the same tiles and roundings as rollout_project_ng, written to a.pre_eps / a.pre_meps
+template <int BLOCK, int NG>
+__device__ __forceinline__ void rollout_pregen_ng(const NoiseArgs& a, int r, double* zA, double* zB, int tid)
+{
+    const int J = a.J, N = a.N, JP = noise_jp(J);
+    const size_t row = (size_t)r * J * N;
+    const double* zs = zA;
+    double* eps = zB;
+    __syncthreads();   // the normals are complete
+    constexpr int NW = BLOCK / 64;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;
+    const int nti = (N + 15) >> 4;
+    const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
+    const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)a.LT, 0, mat_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
+    auto tile_of = [&](int n) {
+        const int round = n / NW, pos = n % NW, cnt = min(NW, nti - round * NW);
+        return round * NW + ((round & 1) ? cnt - 1 - pos : pos);
+    };
+    for (int n = wv; n < nti; n += NW) {
+        const int ti = tile_of(n);
+        double acc[NG];
+        mfma_tile<NG>(rL, N, 16 * ti, min(N, 16 * ti + 16), zs, JP, lane, acc);
+        const int i = 16 * ti + irow;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
+            if (i < N && d < J) {
+                const double e = a.sigma.v[d] * (0.0 + acc[g]);
+                eps[i * JP + d] = e;
+                a.pre_eps[row + (size_t)d * N + i] = e;
+            }
+        }
+    }
+    __syncthreads();
+    for (int ti = wv; ti < nti; ti += NW) {
+        double acc[NG];
+        mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
+        const int i = 16 * ti + irow;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
+            if (i < N && d < J) a.pre_meps[row + (size_t)d * N + i] = acc[g];
+        }
+    }
+}
+
+// the rollout kernel's row from k_pregen's eps and M eps: params = theta + eps into traj (LDS)
+// and HBM, the noise row, x = params + M eps, then the control costs (rollout_control)
+template <int BLOCK>
+__device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
+                                                 int tid)
+{
+    const int J = a.J, N = a.N, Nall = a.Nall, JN = J * N;
+    const size_t row = (size_t)r * JN;
+    double* xs = zA;
+    for (int idx0 = 0; idx0 < JN; idx0 += 4 * BLOCK) {
+        double e[4], mp[4], th[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = min(idx0 + tid + u * BLOCK, JN - 1);
+            e[u] = a.pre_eps[row + idx];
+            mp[u] = a.pre_meps[row + idx];
+            th[u] = a.theta[idx];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = idx0 + tid + u * BLOCK;
+            if (idx < JN) {
+                const int d = idx / N, i = idx - d * N;
+                const double p = th[u] + e[u];
+                traj[idx] = p;
+                a.noise[row + idx] = e[u];
+                a.params[row + idx] = p;
+                xs[d * Nall + i + 6] = p + mp[u];
+            }
+        }
+    }
+    rollout_control<BLOCK>(a, row, xs, zB, tid);
 }
 
 // the engine runs the fused phase for J <= 16 (at most four groups of 4 joint columns)
