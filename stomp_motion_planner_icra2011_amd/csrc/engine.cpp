@@ -81,11 +81,13 @@ struct stomp_engine {
     double *d_mm = nullptr, *d_psum_part = nullptr, *d_psum_all = nullptr, *d_u_part = nullptr, *d_u_all = nullptr;
     int K_gen = 0;
     // pregen (K_r = 0, fused noise phase): the normals, eps = sigma L z and M eps of iteration
-    // it + 1 are made by extra blocks of iteration it's weights launch (on CUs the weights tiles
-    // leave idle); the rollout launch of it + 1 reads them
+    // it + 1 are made by extra low-priority blocks of iteration it's rollout launch (pre_host 1;
+    // or of its weights launch, pre_host 2); the rollout launch of it + 1 reads them.  Two
+    // buffers, by iteration parity: a rollout launch reads one and fills the other.
     bool pre_on = false;
-    int pre_it = -1;                  // iteration whose rows are in d_pre_eps / d_pre_meps (enqueued)
-    double *d_pre_eps = nullptr, *d_pre_meps = nullptr;
+    int pre_host = 1;
+    int pre_it = -1;                  // iteration whose rows are in d_pre_eps / d_pre_meps[it & 1] (enqueued)
+    double *d_pre_eps[2] = {nullptr, nullptr}, *d_pre_meps[2] = {nullptr, nullptr};
     double* h_total = nullptr;
     uint8_t* h_cf = nullptr;
     // eval scratch
@@ -403,7 +405,7 @@ NoiseArgs noise_args(const stomp_engine* e, int it)
     for (int r = 0; r < 3; ++r) na.wr[r] = w * e->smooth[r];
     na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0; na.row_begin = 0;
     na.stop = e->d_stop;
-    na.pre_eps = e->d_pre_eps; na.pre_meps = e->d_pre_meps;
+    na.pre_eps = e->d_pre_eps[it & 1]; na.pre_meps = e->d_pre_meps[it & 1];
     return na;
 }
 
@@ -452,7 +454,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     // every local row generated (K_r = 0): eps and M eps come from k_pregen
     const bool pre = fused && e->pre_on && num_gen == e->K_loc;
     if (pre) {
-        if (e->pre_it != it) {   // not made ahead by the previous iteration's weights launch
+        if (e->pre_it != it) {   // not made ahead by the previous iteration's launches
             Timed tm(e, T_PREGEN);
             launch_pregen(pregen_args(e, it), e->K_loc, e->stream);
         }
@@ -470,6 +472,11 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         ca.nz = na;
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
+        if (pre && e->pre_host == 1) {
+            ca.pre_rows = e->K_loc;
+            ca.pre_next = pregen_args(e, it + 1);
+            e->pre_it = it + 1;
+        }
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
@@ -496,7 +503,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     // the first weights launch carries the next iteration's pregen rows
     NoiseArgs next{};
     const NoiseArgs* carry = nullptr;
-    if (pre) {
+    if (pre && e->pre_host == 2) {
         next = pregen_args(e, it + 1);
         carry = &next;
         e->pre_it = it + 1;
@@ -748,13 +755,17 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         // STOMP_PREGEN=0: the rollout kernel draws its own noise (A/B hook)
         const char* pg = std::getenv("STOMP_PREGEN");
 #ifndef STOMP_SEPARATE_NOISE
-        e->pre_on = e->Kr == 0 && J <= 16 && weights_carry_pregen(e->K_loc) && !(pg && pg[0] == '0');
+        const char* ph = std::getenv("STOMP_PREGEN_HOST");
+        e->pre_host = (ph && std::strcmp(ph, "weights") == 0) ? 2 : 1;
+        e->pre_on = e->Kr == 0 && J <= 16 && (e->pre_host == 1 || weights_carry_pregen(e->K_loc)) &&
+                    !(pg && pg[0] == '0');
 #endif
     }
-    if (e->pre_on) {
-        CREATE_TRY(dev_alloc(e, &e->d_pre_eps, KJN));
-        CREATE_TRY(dev_alloc(e, &e->d_pre_meps, KJN));
-    }
+    if (e->pre_on)
+        for (int b = 0; b < 2; ++b) {
+            CREATE_TRY(dev_alloc(e, &e->d_pre_eps[b], KJN));
+            CREATE_TRY(dev_alloc(e, &e->d_pre_meps[b], KJN));
+        }
     CREATE_TRY(dev_alloc(e, &e->d_x_params, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_noise, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_control, (size_t)J * N));

@@ -101,9 +101,32 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ int flag;
     __shared__ int nz_count;
-    if (a.stop && *a.stop) return;
     const int J = m.J, N = m.N, S = m.S;
     const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
+    {
+        // blocks past the rollouts: the next iteration's pregen rows (normals, sigma L z,
+        // M eps), left at the default wave priority while the rollout waves raise theirs, so
+        // they take the issue slots the latency-bound rollout waves leave idle and the CUs
+        // the early-finishing rollouts free; no stop check (the rows stay valid for pre_it)
+        const int nro = a.num_noisy + (a.x_params ? 1 : 0);
+        if ((int)blockIdx.x >= nro) {
+            const NoiseArgs& pa = a.pre_next;
+            double* pA = (double*)(lds_raw + L.nzA);
+            double* pB = (double*)(lds_raw + L.nzB);
+            const int r = blockIdx.x - nro;
+            rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
+            if (J <= 8) {
+                pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
+                pregen_meps_ng<BLOCK, 2>(pa, r, pB, threadIdx.x);
+            } else {
+                pregen_eps_ng<BLOCK, 4>(pa, r, pA, pB, threadIdx.x);
+                pregen_meps_ng<BLOCK, 4>(pa, r, pB, threadIdx.x);
+            }
+            return;
+        }
+    }
+    if (a.pre_rows > 0) __builtin_amdgcn_s_setprio(2);
+    if (a.stop && *a.stop) return;
     double* traj = (double*)(lds_raw + L.traj);   // J*N
     double* fb = (double*)(lds_raw + L.fb);       // 12*N frame of the current slot
     double* sv = (double*)(lds_raw + L.sv);       // nsaves*12*N saved branch-point frames
@@ -437,8 +460,13 @@ __global__ __launch_bounds__(BLOCK) void k_pregen(NoiseArgs a)
     double* zA = (double*)lds_pg;
     double* zB = (double*)(lds_pg + (L.nzB - L.nzA));
     rollout_normals<BLOCK>(a, blockIdx.x, zA, zB, threadIdx.x);
-    if (a.J <= 8) rollout_pregen_ng<BLOCK, 2>(a, blockIdx.x, zA, zB, threadIdx.x);
-    else rollout_pregen_ng<BLOCK, 4>(a, blockIdx.x, zA, zB, threadIdx.x);
+    if (a.J <= 8) {
+        pregen_eps_ng<BLOCK, 2>(a, blockIdx.x, zA, zB, threadIdx.x);
+        pregen_meps_ng<BLOCK, 2>(a, blockIdx.x, zB, threadIdx.x);
+    } else {
+        pregen_eps_ng<BLOCK, 4>(a, blockIdx.x, zA, zB, threadIdx.x);
+        pregen_meps_ng<BLOCK, 4>(a, blockIdx.x, zB, threadIdx.x);
+    }
 }
 
 void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s)
@@ -485,7 +513,7 @@ int rollout_blocks_per_cu(size_t lds_total)
 
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
-    const int blocks = a.num_noisy + (a.x_params ? 1 : 0);
+    const int blocks = a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
     if (lds > 64 * 1024) {

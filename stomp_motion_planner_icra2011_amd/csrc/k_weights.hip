@@ -415,8 +415,13 @@ __global__ __launch_bounds__(256) void k_weights_rows_pre(WeightArgs a, NoiseArg
     double* zB = (double*)((unsigned char*)V + (L.nzB - L.nzA));
     const int r = blockIdx.x - nw;
     rollout_normals<256>(na, r, zA, zB, threadIdx.x);
-    if (na.J <= 8) rollout_pregen_ng<256, 2>(na, r, zA, zB, threadIdx.x);
-    else rollout_pregen_ng<256, 4>(na, r, zA, zB, threadIdx.x);
+    if (na.J <= 8) {
+        pregen_eps_ng<256, 2>(na, r, zA, zB, threadIdx.x);
+        pregen_meps_ng<256, 2>(na, r, zB, threadIdx.x);
+    } else {
+        pregen_eps_ng<256, 4>(na, r, zA, zB, threadIdx.x);
+        pregen_meps_ng<256, 4>(na, r, zB, threadIdx.x);
+    }
 }
 
 STOMP_STAMP_ACCESSORS(weights)

@@ -159,6 +159,8 @@ struct CostArgs {
     double* total_out;          // [num_noisy] or null
     const double* x_params;     // [J][N] or null
     int x_member;
+    int pre_rows;               // > 0: blocks after the rollouts make k_pregen's rows of pre_next (the
+    NoiseArgs pre_next;         // next iteration) at low priority in the same dispatch
     double* x_state;
     uint8_t* x_cf;
     double* x_traj;
@@ -261,6 +263,8 @@ void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
 // pre: also make the next iteration's k_pregen rows in the same launch (weights_carry_pregen)
 void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre = nullptr);
 bool weights_carry_pregen(int K_loc);
+// where the next iteration's pregen rows ride: 1 = the rollout launch (low-priority blocks),
+// 2 = the weights launch (STOMP_PREGEN_HOST=weights)
 int weights_tile(int K_loc);
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
                    double* theta, const int* stop, hipStream_t s);

@@ -383,10 +383,12 @@ __device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, 
     STAMP(63);
 }
 
-// k_pregen's row: normals (rollout_normals, already issued), eps = sigma_d (0 + L z) and M eps,
-// the same tiles and roundings as rollout_project_ng, written to a.pre_eps / a.pre_meps
+// k_pregen's row, first half: normals (rollout_normals, already issued) and
+// eps = sigma_d (0 + L z), the same tiles and roundings as rollout_project_ng, written to
+// a.pre_eps and (layout [i][JP], for pregen_meps_ng) to the LDS buffer zB.  (M eps as a
+// separate half in the update launch was measured slower: 10.3 us update vs 5.1.)
 template <int BLOCK, int NG>
-__device__ __forceinline__ void rollout_pregen_ng(const NoiseArgs& a, int r, double* zA, double* zB, int tid)
+__device__ __forceinline__ void pregen_eps_ng(const NoiseArgs& a, int r, double* zA, double* zB, int tid)
 {
     const int J = a.J, N = a.N, JP = noise_jp(J);
     const size_t row = (size_t)r * J * N;
@@ -399,7 +401,6 @@ __device__ __forceinline__ void rollout_pregen_ng(const NoiseArgs& a, int r, dou
     const int nti = (N + 15) >> 4;
     const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
     const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc((void*)a.LT, 0, mat_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
     auto tile_of = [&](int n) {
         const int round = n / NW, pos = n % NW, cnt = min(NW, nti - round * NW);
         return round * NW + ((round & 1) ? cnt - 1 - pos : pos);
@@ -419,7 +420,22 @@ __device__ __forceinline__ void rollout_pregen_ng(const NoiseArgs& a, int r, dou
             }
         }
     }
-    __syncthreads();
+}
+
+// second half: M eps from eps in LDS ([i][JP] with zero rows N .. N + kBandBatch and zero
+// columns J .. JP, as rollout_normals leaves them) to a.pre_meps
+template <int BLOCK, int NG>
+__device__ __forceinline__ void pregen_meps_ng(const NoiseArgs& a, int r, const double* eps, int tid)
+{
+    const int J = a.J, N = a.N, JP = noise_jp(J);
+    const size_t row = (size_t)r * J * N;
+    __syncthreads();   // eps is complete
+    constexpr int NW = BLOCK / 64;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;
+    const int nti = (N + 15) >> 4;
+    const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
+    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
     for (int ti = wv; ti < nti; ti += NW) {
         double acc[NG];
         mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
