@@ -306,6 +306,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         return m.nops;
     };
     int op = fk_advance(0);
+    STAMP(7);
     while (op < m.nops) {
         const FkOp o = ops_s[op];
         if (fk_lane) {

@@ -55,11 +55,12 @@ def cost_label(i):
     if 10 <= i < 40:
         g, ph = (i - 10) // 4, (i - 10) % 4
         return f"slot {g}: " + ["FK + publish", "positions+gathers+pots", "velocity", "fold (lanes t<N)"][ph]
-    return {0: "start", 6: "normals / traj + tables", 7: "normals barrier", 8: "L z", 9: "M eps", 1: "control", 2: "joint limits", 3: "traj out",
+    return {0: "start", 6: "normals / traj + tables", 7: "normals barrier | first FK advance", 8: "L z", 9: "M eps", 1: "control", 2: "joint limits", 3: "traj out",
             4: "FK/pairs done", 5: "end"}.get(i, str(i))
 
 
-show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch
+show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch (odd: FK on waves 2-3)
+show("cost", 2, cost_label)   # an even one (FK on waves 0-1, thread 0 stamps inside the FK lanes)
 show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
 show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
 show("weights", 0, lambda i: ["start", "min/max", "exp", "psum", "u partials", "end", "tile loaded"][i])
