@@ -169,6 +169,38 @@ def test_run_matches_iterate():
     np.testing.assert_array_equal(e1.theta(), e2.theta())
 
 
+def test_out_of_order_iterations_bitwise():
+    """The engine makes the next iteration's noise rows ahead (pregen blocks of the rollout
+    launch, ping-pong buffers keyed by iteration parity).  Iteration numbers that skip, repeat
+    or go back, with set_theta / execute calls in between, must discard those rows."""
+    p = make(K=64)
+    o, e = po.Oracle(p), eng.Engine(p)
+    th = o.theta()
+    for it in (1, 2, 5, 6, 6, 3, 10, 12, 11):
+        if it == 3:
+            nt = th + 0.01
+            o.set_theta(nt)
+            e.set_theta(nt)
+        if it == 10:
+            c, cf, _ = e.execute(th[None], iteration_member=4)
+            oc, ocf, _ = o.execute(th, iteration_member=4)
+            np.testing.assert_array_equal(c[0], oc)
+        _compare_iteration(o, e, it)
+
+
+def test_run_chunks_match_iterate():
+    """run() chunks that continue, restart and skip iteration numbers, against iterate()."""
+    p = make(K=128)
+    e1, e2 = eng.Engine(p), eng.Engine(p)
+    seq = [(1, 3), (4, 2), (4, 1), (9, 3)]
+    for first, n in seq:
+        for it in range(first, first + n):
+            e1.iterate(it)
+        e2.run(first, n)
+    e2.synchronize()
+    np.testing.assert_array_equal(e1.theta(), e2.theta())
+
+
 def test_sdf_build_device_bitwise():
     for n in (32, 64, 96):
         p = make(grid_n=n)
