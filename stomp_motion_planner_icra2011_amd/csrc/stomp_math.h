@@ -111,13 +111,13 @@ STOMP_HD void det_sincos(double x, double* s, double* c)
     double hz = 0.5 * z;
     double w = 1.0 - hz;
     double kc = w + (((1.0 - w) - hz) + z * rc);
-    double so, co;
-    if (n == 0) { so = ks; co = kc; }
-    else if (n == 1) { so = kc; co = -ks; }
-    else if (n == 2) { so = -ks; co = -kc; }
-    else { so = -kc; co = ks; }
-    *s = so;
-    *c = co;
+    // quadrant n: (sin, cos) = (ks, kc), (kc, -ks), (-ks, -kc), (-kc, ks), as selects (a
+    // divergent if-chain runs every path under exec masks when the waypoints' quadrants differ)
+    const bool odd = (n & 1) != 0, neg = (n & 2) != 0;
+    const double so = odd ? kc : ks;
+    const double co = odd ? -ks : kc;
+    *s = neg ? -so : so;
+    *c = neg ? -co : co;
 }
 
 // atan: fdlibm s_atan.c (reduction about atan(0.5), atan(1), atan(1.5), atan(inf), hi/lo
