@@ -223,7 +223,7 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
     constexpr int BLOCK = 256, RS = BLOCK / TCW;
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
-    __shared__ double mn_s[TCW], den_s[TCW], ps_s[TCW];
+    __shared__ double ps_s[TCW];
     if (a.stop && *a.stop) return;
     const int N = a.N, J = a.J, K = a.K_loc;
     const int JN = J * N;
@@ -274,50 +274,45 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
                 if (v[k] > lmx) lmx = v[k];
             }
         }
+        double mn, mx;
         if (a.mode == W_PSUM) {
-            if (tid < TCW && colok) {
-                red0[tid] = -a.mm[JN + c];
-                red1[tid] = a.mm[c];
-            }
+            mn = -a.mm[JN + cl];
+            mx = a.mm[cl];
         } else {
-            red0[tid] = lmn;
-            red1[tid] = lmx;
+            // min / max over the lanes holding the same column (lane xor TCW, 2 TCW, .. 32),
+            // then over the four waves through LDS; order-free, so any tree is exact
+#pragma unroll
+            for (int off = TCW; off < 64; off <<= 1) {
+                const double omn = __shfl_xor(lmn, off, 64), omx = __shfl_xor(lmx, off, 64);
+                if (omn < lmn) lmn = omn;
+                if (omx > lmx) lmx = omx;
+            }
+            const int lane = tid & 63, wv = tid >> 6;
+            if (lane < TCW) {
+                red0[wv * TCW + lane] = lmn;
+                red1[wv * TCW + lane] = lmx;
+            }
             __syncthreads();
-            if (tid < TCW) {
-                double mn = red0[tid], mx = red1[tid];
-                for (int j0 = tid + TCW; j0 < BLOCK; j0 += 16 * TCW) {
-                    double x0[16], x1[16];
+            mn = red0[cc];
+            mx = red1[cc];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) {
-                        const int j = min(j0 + q * TCW, BLOCK - TCW + tid);   // stays in this column
-                        x0[q] = red0[j];
-                        x1[q] = red1[j];
-                    }
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) {   // order-free; the clamped repeats are harmless
-                        if (x0[q] < mn) mn = x0[q];
-                        if (x1[q] > mx) mx = x1[q];
-                    }
-                }
-                red0[tid] = mn;
-                red1[tid] = mx;
-                if (a.mode == W_MINMAX && colok) {
+            for (int w = 1; w < BLOCK / 64; ++w) {
+                const double x0 = red0[w * TCW + cc], x1 = red1[w * TCW + cc];
+                if (x0 < mn) mn = x0;
+                if (x1 > mx) mx = x1;
+            }
+            if (a.mode == W_MINMAX) {
+                if (tid < TCW && colok) {
                     a.mm[c] = mx;
                     a.mm[JN + c] = -mn;
                 }
+                return;
             }
-            if (a.mode == W_MINMAX) return;
         }
-        __syncthreads();
-        if (tid < TCW) {
-            double den = red1[tid] - red0[tid];
-            if (den < 1e-8) den = 1e-8;
-            den_s[tid] = den;
-            mn_s[tid] = red0[tid];
-        }
-        __syncthreads();
+        double den = mx - mn;
+        if (den < 1e-8) den = 1e-8;
         STAMP(1);
-        const double mn = mn_s[cc], den = den_s[cc];
+
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const int r = rs + RS * k;
