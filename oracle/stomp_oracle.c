@@ -226,14 +226,25 @@ static void frame_apply(const frame_t* f, const double* v, double* out)
         out[i] = f->R[3 * i + 0] * v[0] + f->R[3 * i + 1] * v[1] + f->R[3 * i + 2] * v[2] + f->p[i];
 }
 
+/* The segment's fixed rotation is exactly the identity (every PR2 segment): KDL's products
+ * with it (rot * Rot2, parent.M * rot) return their other factor up to the sign of zero
+ * entries, and both the oracle and the engine skip them. */
+static int so_rot_identity(const double* r)
+{
+    return r[0] == 1.0 && r[1] == 0.0 && r[2] == 0.0 && r[3] == 0.0 && r[4] == 1.0 && r[5] == 0.0 &&
+           r[6] == 0.0 && r[7] == 0.0 && r[8] == 1.0;
+}
+
 /* segment pose(q) composed onto the parent frame */
 static void segment_frame(const so_segment* s, const frame_t* parent, double q, frame_t* out)
 {
     frame_t pose;
+    const int ident = so_rot_identity(s->rot);
     if (s->q_index >= 0) {
         double Rq[9];
         rot2(s->axis, q, Rq);
-        rotmul(s->rot, Rq, pose.R);
+        if (ident) memcpy(pose.R, Rq, sizeof pose.R);
+        else rotmul(s->rot, Rq, pose.R);
     } else {
         memcpy(pose.R, s->rot, sizeof pose.R);
     }
@@ -242,7 +253,8 @@ static void segment_frame(const so_segment* s, const frame_t* parent, double q, 
         *out = pose;
         return;
     }
-    rotmul(parent->R, pose.R, out->R);
+    if (s->q_index < 0 && ident) memcpy(out->R, parent->R, sizeof out->R);
+    else rotmul(parent->R, pose.R, out->R);
     for (int i = 0; i < 3; ++i)
         out->p[i] = parent->R[3 * i + 0] * pose.p[0] + parent->R[3 * i + 1] * pose.p[1] +
                     parent->R[3 * i + 2] * pose.p[2] + parent->p[i];
@@ -379,7 +391,8 @@ int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, 
         if (j >= 0) {
             double Rq[9];
             rot2(sg->axis, qv, Rq);
-            rotmul(sg->rot, Rq, R);
+            if (so_rot_identity(sg->rot)) memcpy(R, Rq, sizeof(double) * 9);
+            else rotmul(sg->rot, Rq, R);
         } else {
             memcpy(R, sg->rot, sizeof(double) * 9);
         }

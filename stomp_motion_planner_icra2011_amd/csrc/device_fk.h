@@ -46,7 +46,12 @@ __device__ __forceinline__ void compose(const DevSegment& sg, const Frame* paren
         Rq[6] = -m_st_1 + m_vt_0_2;
         Rq[7] = m_st_0 + m_vt_1_2;
         Rq[8] = ct + m_vt_2 * a[2];
-        rotmul(sg.rot, Rq, pose.R);
+        if (sg.rot_identity) {   // rot * Rq with rot = 1 is Rq (up to the sign of zeros; the oracle skips it too)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) pose.R[k] = Rq[k];
+        } else {
+            rotmul(sg.rot, Rq, pose.R);
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 9; ++k) pose.R[k] = sg.rot[k];
@@ -57,7 +62,12 @@ __device__ __forceinline__ void compose(const DevSegment& sg, const Frame* paren
         out = pose;
         return;
     }
-    rotmul(parent->R, pose.R, out.R);
+    if (sg.q_index < 0 && sg.rot_identity) {   // parent * 1
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out.R[k] = parent->R[k];
+    } else {
+        rotmul(parent->R, pose.R, out.R);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
         out.p[i] = parent->R[3 * i + 0] * pose.p[0] + parent->R[3 * i + 1] * pose.p[1] +

@@ -702,6 +702,11 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         const stomp_segment& g = d->segments[s];
         segs[s].parent = g.parent; segs[s].q_index = g.q_index;
         std::memcpy(segs[s].rot, g.rot, sizeof g.rot);
+        // as the oracle's so_rot_identity: products with it are skipped on both sides
+        segs[s].rot_identity = g.rot[0] == 1.0 && g.rot[1] == 0.0 && g.rot[2] == 0.0 && g.rot[3] == 0.0 &&
+                               g.rot[4] == 1.0 && g.rot[5] == 0.0 && g.rot[6] == 0.0 && g.rot[7] == 0.0 &&
+                               g.rot[8] == 1.0;
+        segs[s].pad_ = 0;
         std::memcpy(segs[s].trans, g.trans, sizeof g.trans);
         std::memcpy(segs[s].axis, g.axis, sizeof g.axis);
     }

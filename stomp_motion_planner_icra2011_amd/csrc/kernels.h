@@ -40,6 +40,7 @@ constexpr int kBaseRoot = -1;
 
 struct DevSegment {
     int parent, q_index;
+    int rot_identity, pad_;     // the fixed rotation is exactly the identity: its products are skipped
     double rot[9];
     double trans[3];
     double axis[3];
