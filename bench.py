@@ -66,6 +66,25 @@ def latest_traffic():
         return None
 
 
+def cpu_baseline_all_cores(problem, budget_s: float):
+    """SURVEY.md 8(d)'s stronger CPU baseline: the oracle with banded stencils and Task::execute
+    spread over the host cores this process may use (OpenMP over rollouts)."""
+    from oracle import pyoracle as po
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    o = po.Oracle(problem, dense=False, threads=threads)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        o.iterate(n + 1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 400:
+            break
+    return {"value": n / el, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} iterations of the same workload on the CPU oracle with banded stencils and "
+                      f"OpenMP over the rollouts' Task::execute, {threads} threads, {el:.1f} s"}
+
+
 def cfg_name(args, world: int) -> str:
     """The BASELINE.json config a run's shape matches, or "custom"."""
     shape = (args.dof, args.waypoints, args.rollouts_per_gpu * world, args.grid, args.problems)
@@ -260,11 +279,12 @@ def main():
             optimize = {"iterations": st.iterations, "iterations_per_s": round(st.iterations / dt, 3)}
             eo.close()
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         pc = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
                              num_reused_rollouts=0)
         cpu = cpu_baseline(pc, args.cpu_seconds)
+        cpu_mt = cpu_baseline_all_cores(pc, min(args.cpu_seconds, 8.0))
 
     if rank == 0:
         out = {
@@ -279,6 +299,7 @@ def main():
                        "rollouts_per_s": round(value * K, 1)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_mt,
             "kernel_timing_us": {k: round(v["avg_us"], 3) for k, v in timing.items()},
             "optimize_loop": optimize,
         }

@@ -1290,10 +1290,22 @@ static void generate_rollouts(so_problem* P, int iteration_number, const double*
         }
         free(v);
     }
-    double* z = dalloc((size_t)N);
-    double* tmp = dalloc((size_t)N);
-    for (int d = 0; d < J; ++d)
-        for (int r = 0; r < P->K_gen; ++r) {
+    /* d outer, r inner in the reference; the (d, r) samples are independent (counter-based
+     * normals), so the threads of a multi-core run may take them in any order */
+    const int K_gen = P->K_gen;
+    int nthreads = P->cfg.threads > 0 ? P->cfg.threads : 1;
+    (void)nthreads;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        double* z = dalloc((size_t)N);
+        double* tmp = dalloc((size_t)N);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (int dr = 0; dr < J * K_gen; ++dr) {
+            const int d = dr / K_gen, r = dr % K_gen;
             so_normals(P->cfg.seed, iteration_number, d, r, N, z);
             /* MultivariateGaussian::sample: output = mean + L * z (multivariate_gaussian.h:88-94) */
             matvec_fma(P->L, N, z, tmp, !P->cfg.dense);
@@ -1304,8 +1316,9 @@ static void generate_rollouts(so_problem* P, int iteration_number, const double*
                 pr[t] = P->theta[(size_t)d * N + t] + nz[t];
             }
         }
-    free(z);
-    free(tmp);
+        free(z);
+        free(tmp);
+    }
 }
 
 /* fixed-order blocked sum over rollouts; returns sum_r vals[r*stride] */
@@ -1331,14 +1344,17 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
     for (int d = 0; d < J; ++d) sigma[d] = P->cfg.noise_stddev[d] * pow(P->cfg.noise_decay[d], iteration_number - 1);
     generate_rollouts(P, iteration_number, sigma);
     free(sigma);
-    /* computeProjectedNoise for all K (policy_improvement.cpp:283-290, 473-482) */
+    int nthreads = P->cfg.threads > 0 ? P->cfg.threads : 1;
+    (void)nthreads;
+    /* computeProjectedNoise for all K (policy_improvement.cpp:283-290, 473-482); rows independent */
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+#endif
     for (int r = 0; r < K; ++r)
         for (int d = 0; d < J; ++d)
             matvec_fma(P->M, N, P->r_noise + r * JN + (size_t)d * N, P->r_nproj + r * JN + (size_t)d * N, 0);
 
     /* Task::execute for each generated rollout (policy_improvement_loop.cpp:165-170) */
-    int nthreads = P->cfg.threads > 0 ? P->cfg.threads : 1;
-    (void)nthreads;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads)
 #endif
@@ -1356,10 +1372,16 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
     }
 
     /* setRolloutCosts -> computeRolloutControlCosts for all K (policy_improvement.cpp:262-281) */
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
     {
         double* xall = dalloc((size_t)Nall);
         double* call = dalloc((size_t)Nall);
         double w = 0.5 * P->cfg.smoothness_cost_weight;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
         for (int r = 0; r < K; ++r) control_costs(P, P->r_params + r * JN, P->r_nproj + r * JN, w, P->r_ctrl + r * JN, xall, call);
         free(xall);
         free(call);
