@@ -34,6 +34,17 @@ __device__ __forceinline__ double lds_seq_sum(const double* p, int stride, int c
     return s;
 }
 
+// The rows kernel's LDS tile V: row r of column cc at r * TCW + cc, each 64-row summation
+// block shifted by kVPad doubles so that the block-sum threads (one per block and column,
+// reading row q of their block together) hit distinct banks: without the shift the blocks
+// are 64 * TCW * 8 B apart, a multiple of the 256-B bank row, and all land on one bank.
+constexpr int kVPad = 4;
+__device__ __forceinline__ int vidx(int r, int cc, int tcw) { return r * tcw + cc + (r / kSumBlock) * kVPad; }
+__host__ __device__ inline size_t weights_rows_v_bytes(int K_loc, int tcw)
+{
+    return ((size_t)K_loc * tcw + (size_t)((K_loc + kSumBlock - 1) / kSumBlock) * kVPad) * sizeof(double);
+}
+
 // EPT: cost-tile elements per lane, K_loc * TC <= EPT * 256
 template <int EPT>
 __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
@@ -317,14 +328,14 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
         for (int k = 0; k < EPT; ++k) {
             const int r = rs + RS * k;
             v[k] = det_exp(-10.0 * (v[k] - mn) / den);
-            if (r < K) V[r * TCW + cc] = v[k];
+            if (r < K) V[vidx(r, cc, TCW)] = v[k];
         }
         __syncthreads();
         STAMP(2);
         if (tid < nb * TCW) {
             const int b = tid / TCW, c2 = tid % TCW;
             const int r1 = min(K, (b + 1) * kSumBlock);
-            const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TCW + c2, TCW, r1 - b * kSumBlock);
+            const double s = lds_seq_sum(V + vidx(b * kSumBlock, c2, TCW), TCW, r1 - b * kSumBlock);
             part[tid] = s;
             if (a.mode == W_PSUM && c0 + c2 < JN) a.psum_part[(size_t)b * JN + c0 + c2] = s;
         }
@@ -360,17 +371,17 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
         for (int k = 0; k < EPT; ++k) {
             const int r = rs + RS * k;
             if (r >= K) continue;
-            if (!colok) { V[r * TCW + cc] = 0.0; continue; }
+            if (!colok) { V[vidx(r, cc, TCW)] = 0.0; continue; }
             const double pn = v[k] / ps;
             a.prob[(size_t)r * JN + c] = pn;
-            V[r * TCW + cc] = nz[k] * pn;
+            V[vidx(r, cc, TCW)] = nz[k] * pn;
         }
     }
     __syncthreads();
     if (tid < nb * TCW) {
         const int b = tid / TCW, c2 = tid % TCW;
         const int r1 = min(K, (b + 1) * kSumBlock);
-        const double s = lds_seq_sum(V + (size_t)b * kSumBlock * TCW + c2, TCW, r1 - b * kSumBlock);
+        const double s = lds_seq_sum(V + vidx(b * kSumBlock, c2, TCW), TCW, r1 - b * kSumBlock);
         part[tid] = s;
         if (a.mode == W_USUM && c0 + c2 < JN) a.u_part[(size_t)b * JN + c0 + c2] = s;
     }
@@ -442,7 +453,7 @@ static void launch_rows(const WeightArgs& a, const NoiseArgs* pre, hipStream_t s
     constexpr int TCW = WEIGHTS_ROWS_TCW;
     const int JN = a.J * a.N;
     const int nw = (JN + TCW - 1) / TCW;
-    size_t lds = (size_t)a.K_loc * TCW * sizeof(double);
+    size_t lds = weights_rows_v_bytes(a.K_loc, TCW);
     if (pre) {
         const RolloutLds L = rollout_lds(pre->J, pre->N, 0, 0, 0, 0, 0, 0, 0);
         const size_t lp = 2 * (size_t)(L.nzB - L.nzA);
