@@ -175,6 +175,13 @@ def bench_problems(args, world, rank, local_rank, dist):
 
 def main():
     args = parse()
+    if args.problems > 1:
+        # one stream per problem: give HIP as many hardware queues as it needs to run them side by
+        # side (its default, 4, puts several problems' launches in one in-order queue; measured
+        # 24.9k -> 36.4k problem-iterations/s at 8 problems).  Set before the runtime initialises.
+        want = min(32, max(4, 2 * args.problems))
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
