@@ -45,6 +45,11 @@ __host__ __device__ inline size_t weights_rows_v_bytes(int K_loc, int tcw)
     return ((size_t)K_loc * tcw + (size_t)((K_loc + kSumBlock - 1) / kSumBlock) * kVPad) * sizeof(double);
 }
 
+#ifndef WEIGHTS_ROWS_BLOCK
+#define WEIGHTS_ROWS_BLOCK 256
+#endif
+constexpr int kWRB = WEIGHTS_ROWS_BLOCK;   // threads of a rows-kernel workgroup
+
 // EPT: cost-tile elements per lane, K_loc * TC <= EPT * 256
 template <int EPT>
 __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
 template <int TCW, int EPT>
 __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int nt, double* V)
 {
-    constexpr int BLOCK = 256, RS = BLOCK / TCW;
+    constexpr int BLOCK = kWRB, RS = BLOCK / TCW;
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
     __shared__ double ps_s[TCW];
@@ -397,7 +402,7 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
 }
 
 template <int TCW, int EPT>
-__global__ __launch_bounds__(256) void k_weights_rows(WeightArgs a)
+__global__ __launch_bounds__(kWRB) void k_weights_rows(WeightArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double V[];   // [K_loc][TCW]
     weights_rows<TCW, EPT>(a, blockIdx.x, gridDim.x, V);
@@ -473,15 +478,15 @@ static void launch_rows(const WeightArgs& a, const NoiseArgs* pre, hipStream_t s
                                   (int)lds);
         raised = lds;
     }
-    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(kWRB), lds, s, a);
 }
 
 bool weights_carry_pregen(int K_loc)
 {
 #ifndef WEIGHTS_COLUMN_TILES
-    constexpr int RS = 256 / WEIGHTS_ROWS_TCW;
+    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
     const int nb = (K_loc + kSumBlock - 1) / kSumBlock;
-    return nb * WEIGHTS_ROWS_TCW <= 256 && K_loc <= 32 * RS;
+    return kWRB == 256 && nb * WEIGHTS_ROWS_TCW <= 256 && K_loc <= 32 * RS;
 #else
     return false;
 #endif
@@ -491,9 +496,9 @@ void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre)
 {
 #ifndef WEIGHTS_COLUMN_TILES
     // row-coalesced flat-column tiles while a lane's rows fit its registers
-    constexpr int RS = 256 / WEIGHTS_ROWS_TCW;
+    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
     const int nb = (a.K_loc + kSumBlock - 1) / kSumBlock;
-    if (nb * WEIGHTS_ROWS_TCW <= 256) {
+    if (nb * WEIGHTS_ROWS_TCW <= kWRB && (kWRB == 256 || !pre)) {
         if (a.K_loc <= 4 * RS) return launch_rows<4>(a, pre, s);
         if (a.K_loc <= 8 * RS) return launch_rows<8>(a, pre, s);
         if (a.K_loc <= 16 * RS) return launch_rows<16>(a, pre, s);
