@@ -118,8 +118,8 @@ def cpu_baseline(problem, budget_s: float):
 
 def bench_problems(args, world, rank, local_rank, dist):
     """cfg5: independent planning problems per GPU (distinct start / goal / seed, one shared
-    device-built SDF), one engine and one stream each, no communication (replicas); the steps
-    are enqueued round-robin over the engines so the streams run concurrently.  value =
+    device-built SDF), one engine and one stream each, no communication (replicas); each
+    engine's steps are enqueued as one run and the streams run concurrently.  value =
     problem-iterations per second over all ranks."""
     from stomp_motion_planner_icra2011_amd import engine as eng
     from stomp_motion_planner_icra2011_amd import problem as pb
@@ -139,9 +139,11 @@ def bench_problems(args, world, rank, local_rank, dist):
         engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr))
 
     def sweep(first, count):
-        for k in range(count):
-            for e in engines:
-                e.run(first + k, 1)
+        # each problem's iterations as one stomp_engine_run (its noiseless rollouts ride in the
+        # next rollout launch; a run of one iteration would flush each as its own launch); the
+        # problems' streams overlap on the device while the host enqueues the next problem
+        for e in engines:
+            e.run(first, count)
         for e in engines:
             e.synchronize()
 
