@@ -181,6 +181,9 @@ int stomp_engine_get_theta(stomp_engine* e, double* theta);
 int stomp_engine_set_theta(stomp_engine* e, const double* theta);
 
 int stomp_engine_iterate(stomp_engine* e, int32_t iteration_number, stomp_iter_out* out);
+/* run: count iterations enqueued with no host sync.  The last one's noiseless rollout is left
+ * pending (it rides in the next rollout launch); synchronize, iterate, set_theta and the
+ * trajectory reads evaluate it first. */
 int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count);
 int stomp_engine_synchronize(stomp_engine* e);
 

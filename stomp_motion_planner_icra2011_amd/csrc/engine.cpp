@@ -976,6 +976,7 @@ int stomp_engine_get_theta(stomp_engine* e, double* theta)
 
 int stomp_engine_set_theta(stomp_engine* e, const double* theta)
 {
+    flush_noiseless(e);   // a pending noiseless rollout belongs to the theta being replaced
     HIP_TRY(e, hipMemcpyAsync(e->d_theta, theta, sizeof(double) * e->J * e->N, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
@@ -1000,16 +1001,18 @@ int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
 
 int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count)
 {
+    // the last iteration's noiseless rollout stays pending: it rides in the next rollout
+    // launch, or is flushed by synchronize, iterate, set_theta and the trajectory reads
     for (int i = 0; i < count; ++i) {
         int rc = enqueue_iteration(e, first_iteration + i, true);
         if (rc) return rc;
     }
-    flush_noiseless(e);
     return 0;
 }
 
 int stomp_engine_synchronize(stomp_engine* e)
 {
+    flush_noiseless(e);
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
 }
@@ -1137,6 +1140,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
 
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
 {
+    flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_best_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
@@ -1144,6 +1148,7 @@ int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
 
 int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj)
 {
+    flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_last_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;

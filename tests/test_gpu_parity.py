@@ -199,6 +199,22 @@ def test_run_chunks_match_iterate():
         e2.run(first, n)
     e2.synchronize()
     np.testing.assert_array_equal(e1.theta(), e2.theta())
+    # run leaves its last noiseless rollout pending: a trajectory read evaluates it, and so does
+    # set_theta before replacing the theta it belongs to
+    e1.iterate(12)
+    e2.run(12, 1)
+    np.testing.assert_array_equal(e1.last_trajectory(), e2.last_trajectory())
+    e1.iterate(13)
+    e2.run(13, 1)
+    th = e1.theta()
+    e2.set_theta(th + 0.02)
+    e1.set_theta(th + 0.02)
+    np.testing.assert_array_equal(e1.last_trajectory(), e2.last_trajectory())
+    e1.iterate(14)
+    e2.run(14, 1)
+    e2.synchronize()
+    np.testing.assert_array_equal(e1.theta(), e2.theta())
+    np.testing.assert_array_equal(e1.last_trajectory(), e2.last_trajectory())
 
 
 def test_sdf_build_device_bitwise():
