@@ -183,6 +183,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     if (tid == 0) flag = 0;
     __syncthreads();
     STAMP(1);
+    BLOCK_MARK(4);
 
     // ---- handleJointLimits
     int any = 0;
@@ -244,6 +245,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         __syncthreads();
     }
     STAMP(2);
+    BLOCK_MARK(5);
     double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
     if (tout)
         for (int idx = tid; idx < J * N; idx += BLOCK) tout[idx] = traj[idx];

@@ -22,7 +22,7 @@ static __device__ int g_stamp_block;
     } while (0)
 // Per-workgroup residency record: {HW_ID, XCC_ID, start, end} for blocks < 8192, to measure
 // how many workgroups of a launch actually share a CU.
-static __device__ unsigned long long g_blocks[8192][4];
+static __device__ unsigned long long g_blocks[8192][6];
 #define BLOCK_BEGIN()                                                                                   \
     do {                                                                                                \
         if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                    \
@@ -39,6 +39,15 @@ static __device__ unsigned long long g_blocks[8192][4];
             unsigned long long _t;                                                                      \
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
             g_blocks[blockIdx.x][3] = _t;                                                               \
+        }                                                                                               \
+    } while (0)
+// per-block phase mark k (4 or 5): the shader clock when thread 0 passes it
+#define BLOCK_MARK(k)                                                                                   \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {                                                    \
+            unsigned long long _t;                                                                      \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                  \
+            g_blocks[blockIdx.x][(k)] = _t;                                                             \
         }                                                                                               \
     } while (0)
 #define STOMP_STAMP_ACCESSORS(name)                                                                     \
@@ -65,6 +74,9 @@ static __device__ unsigned long long g_blocks[8192][4];
     } while (0)
 #define BLOCK_END() \
     do {            \
+    } while (0)
+#define BLOCK_MARK(k) \
+    do {              \
     } while (0)
 #define STOMP_STAMP_ACCESSORS(name)
 #endif

@@ -71,7 +71,7 @@ def residency():
     """Workgroups of one rollout-cost launch per CU, and their overlap in time."""
     fn = lib.stomp_debug_blocks_cost
     fn.argtypes = [C.c_void_p]
-    buf = np.zeros((8192, 4), np.uint64)
+    buf = np.zeros((8192, 6), np.uint64)
     e.run(7, 1)
     e.synchronize()
     fn(buf.ctypes.data)
@@ -90,6 +90,23 @@ def residency():
             cur += d
             mx = max(mx, cur)
         conc.append(mx)
+    # durations by how many rollout WGs their CU ran concurrently (at their start)
+    by_conc = collections.defaultdict(list)
+    for i in range(len(b)):
+        c = int(cu[i])
+        n_at = sum(1 for (a0, a1) in per[c] if a0 <= t0[i] < a1)
+        by_conc[n_at].append(int(t1[i] - t0[i]))
+    for k in sorted(by_conc):
+        v = np.array(by_conc[k])
+        print(f"    CU running {k} rollout WGs at start: {len(v)} WGs, duration mean {int(v.mean())} max {int(v.max())}")
+    ctl, jl = b[:, 4] - t0, b[:, 5] - b[:, 4]
+    rest = t1 - b[:, 5]
+    dur = t1 - t0
+    for name, v in (("start..control", ctl), ("joint limits", jl), ("FK/pairs/fold/end", rest)):
+        print(f"    {name:18s} min/median/max {int(v.min())}/{int(np.median(v))}/{int(v.max())}  "
+              f"corr with duration {np.corrcoef(v, dur)[0, 1]:.2f}")
+    slow = np.argsort(-(t1 - t0))[:8]
+    print("    slowest blocks:", [(int(i), int(t1[i] - t0[i]), len(per[int(cu[i])])) for i in slow])
     span = int(t1.max() - t0.min())
     print(f"--- residency: {len(per)} CUs used by {len(b)} workgroups; per CU: "
           f"{collections.Counter(len(v) for v in per.values())}; max concurrent per CU: {collections.Counter(conc)}")
