@@ -868,8 +868,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     DevModel& m = e->model;
     m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size(); m.nseg = e->nseg;
     m.nslots = e->nslots;
-    m.sph_chunk = 1;   // the per-slot a buffer holds the largest slot
-    for (int g = 0; g < e->nslots; ++g) m.sph_chunk = std::max(m.sph_chunk, slot_sph[g + 1] - slot_sph[g]);
+    m.sph_chunk = 1;   // the a-value buffer holds the longest sphere run
+    for (const FkOp& o : e->ops) m.sph_chunk = std::max(m.sph_chunk, o.sph_end - o.sph_begin);
     {
         if (m.sph_chunk * N > 65535)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "%d spheres on one segment x %d waypoints exceed 16-bit pair ids",

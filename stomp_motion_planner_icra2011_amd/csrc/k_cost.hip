@@ -303,11 +303,12 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         for (; op < m.nops; ++op) {
             const FkOp o = ops_s[op];
             fk_op(o);
-            if (o.slot >= 0) return op;
+            if (o.sph_end > o.sph_begin) return op;   // a run of spheres on C
         }
         return m.nops;
     };
     int op = fk_advance(0);
+    int run = 0;   // sphere runs done (stamp index only)
     STAMP(7);
     while (op < m.nops) {
         const FkOp o = ops_s[op];
@@ -319,8 +320,11 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
         if (tid == 0) nz_count = 0;
         __syncthreads();   // frame published; every lane's previous fold is done
-        STAMP(10 + 4 * o.slot);
-        const int sb = slot_sph_s[o.slot], se = slot_sph_s[o.slot + 1];
+        STAMP(10 + 4 * run);
+        // one run of the slot's spheres (all of them, or run_max(N) at a time: the a-value
+        // buffer and the pair list hold one run); runs of a slot follow in sphere order and
+        // re-publish the same frame
+        const int sb = o.sph_begin, se = o.sph_end;
         const int ns = se - sb;
         int next = -1;
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                         x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
                     dv[u] = sdf_distance(m, x);
                 }
-                STAMP(40 + o.slot);
+                STAMP(40 + run);
 #ifdef FK_PIPELINE
                 // while the first gathers are in flight, lanes t < N run the FK program on to
                 // the next slot's frame (C; the published frame stays in fb for this slot).
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
             }
         }
         __syncthreads();   // pots and the non-zero list complete
-        STAMP(11 + 4 * o.slot);
+        STAMP(11 + 4 * run);
         // velocities only for the listed pairs, spread densely over the block
         for (int i = tid; i < nz_count; i += BLOCK) {
             const int it = nzl[i];
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
 #endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
-        STAMP(12 + 4 * o.slot);
+        STAMP(12 + 4 * run);
         if (fk_lane) {
             // fold in sphere order; the LDS reads go out 16 at a time
             const int nsl = se - sb;
@@ -412,7 +416,8 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         // program's control flow is uniform, so every lane arrives at the same next op
         if (next < 0) next = fk_advance(op + 1);
         op = next;
-        STAMP(13 + 4 * o.slot);
+        STAMP(13 + 4 * run);
+        ++run;
     }
     STAMP(4);
     if (col) flag = 1;   // every writer stores 1

@@ -18,8 +18,8 @@
 namespace stomp {
 
 constexpr int kMaxJoints = 32;
-constexpr int kRunMaxSmall = 12;  // spheres per FK op when N <= 128 (LDS batch)
-constexpr int kRunMaxLarge = 8;   // spheres per FK op when N > 128
+constexpr int kRunMaxSmall = 16;  // spheres per run (one a-value buffer of the rollout kernel) when N <= 128
+constexpr int kRunMaxLarge = 8;   // when N > 128: keeps two rollout WGs per CU at N = 199
 constexpr int kSaves = 2;         // saved branch-point FK frames (LDS, one column per waypoint)
 constexpr int kSumBlock = 64;     // canonical blocked summation over rollouts
 constexpr int kBandBatch = 8;     // rows per load batch of the noise band products
