@@ -234,7 +234,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = args.steps / elapsed
+    global_its = args.steps / elapsed
+    # The metric's unit is a K = 512 iteration (BASELINE.json).  With K = 512 per GPU the N-GPU
+    # run does one K = 512 N iteration per step, i.e. N units of the metric's work, so the
+    # whole-job aggregate is N x the global iteration rate (at N = 1 the two are the same).
+    value = global_its * world
 
     # Kernel durations: the same K steps again with HIP events recorded around every stage
     # on the engine stream.  The events themselves cost ~10 us of dispatch gap per stage,
@@ -269,7 +273,7 @@ def main():
         # whole iteration, B_iter = E * N * (4 S + 16 J + 8), E = K + 1, all ranks
         b_iter = (K + 1) * p.N * (4 * S + 16 * p.J + 8)
         roofline["iteration_bytes"] = b_iter
-        roofline["iteration_frac"] = round(b_iter * value / (HBM_PEAK_GBS * 1e9 * world), 5)   # vs N x peak
+        roofline["iteration_frac"] = round(b_iter * global_its / (HBM_PEAK_GBS * 1e9 * world), 5)   # vs N x peak
 
     # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
     # the same iterations with the optimizer's bookkeeping, no early stop
@@ -305,7 +309,10 @@ def main():
                                    f"(K={K} total), K_r=0, {args.grid}^3 SDF, S={S} spheres",
                        "rollouts_per_gpu": args.rollouts_per_gpu, "global_rollouts": K,
                        "parallelism": f"rollout shard x{world}" + (" (RCCL)" if world > 1 else ""),
-                       "rollouts_per_s": round(value * K, 1)},
+                       "global_iterations_per_s": round(global_its, 3),
+                       "value_unit": f"iterations of K={args.rollouts_per_gpu} per second, summed over GPUs "
+                                     f"(= global K={K} iterations/s x {world})",
+                       "rollouts_per_s": round(global_its * K, 1)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,
