@@ -112,6 +112,17 @@ struct stomp_engine {
 
 namespace {
 
+// a communicator exists: world > 1, or the one-rank RCCL hook
+bool has_comm(const stomp_engine* e)
+{
+#ifdef STOMP_WITH_RCCL
+    return e->comm != nullptr;
+#else
+    (void)e;
+    return false;
+#endif
+}
+
 int fail(stomp_engine* e, int code, const char* fmt, ...)
 {
     char buf[512];
@@ -522,25 +533,25 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             wa.mode = W_MINMAX;
             launch_weights(wa, e->stream, carry);
 #ifdef STOMP_WITH_RCCL
-            if (e->world > 1)
+            if (e->comm)
                 NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
 #endif
             wa.mode = W_PSUM;
             launch_weights(wa, e->stream);
 #ifdef STOMP_WITH_RCCL
-            if (e->world > 1)
+            if (e->comm)
                 NCCL_TRY(e, ncclAllGather(e->d_psum_part, e->d_psum_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
 #endif
-            if (e->world == 1)
+            if (!has_comm(e))
                 HIP_TRY(e, hipMemcpyAsync(e->d_psum_all, e->d_psum_part, sizeof(double) * nb_loc * JN,
                                           hipMemcpyDeviceToDevice, e->stream));
             wa.mode = W_USUM;
             launch_weights(wa, e->stream);
 #ifdef STOMP_WITH_RCCL
-            if (e->world > 1)
+            if (e->comm)
                 NCCL_TRY(e, ncclAllGather(e->d_u_part, e->d_u_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
 #endif
-            if (e->world == 1)
+            if (!has_comm(e))
                 HIP_TRY(e, hipMemcpyAsync(e->d_u_all, e->d_u_part, sizeof(double) * nb_loc * JN,
                                           hipMemcpyDeviceToDevice, e->stream));
         }
@@ -953,6 +964,15 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         std::memcpy(&id, d->comm_id, sizeof id);
         if (ncclCommInitRank(&e->comm, world, id, e->rank) != ncclSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "ncclCommInitRank failed"));
+    } else if (e->split_modes) {
+        // STOMP_DEBUG_RCCL_ONE_RANK=1 (with the sharded-modes hook): a one-rank communicator,
+        // so the sharded path's RCCL all-reduce / all-gathers run on a one-GPU box
+        const char* one = std::getenv("STOMP_DEBUG_RCCL_ONE_RANK");
+        if (one && one[0] == '1') {
+            ncclUniqueId id;
+            if (ncclGetUniqueId(&id) != ncclSuccess || ncclCommInitRank(&e->comm, 1, id, 0) != ncclSuccess)
+                CREATE_TRY(fail(e, STOMP_E_COMM, "one-rank ncclCommInitRank failed"));
+        }
     }
 #endif
     if (hipStreamSynchronize(e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "setup failed"));

@@ -137,6 +137,21 @@ def test_sharded_weight_phases_bitwise(monkeypatch, K, cum):
         _compare_iteration(o, e, it)
 
 
+def test_sharded_weight_phases_through_rccl_bitwise(monkeypatch):
+    # the same decomposition with the collectives issued through RCCL on a one-rank
+    # communicator (ncclAllReduce max, two ncclAllGather), as the multi-GPU engine issues them
+    monkeypatch.setenv("STOMP_DEBUG_SHARDED_MODES", "1")
+    monkeypatch.setenv("STOMP_DEBUG_RCCL_ONE_RANK", "1")
+    p = make(K=128, Kr=0)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+    e.run(4, 20)
+    for it in range(4, 24):
+        o.iterate(it)
+    np.testing.assert_array_equal(e.theta(), o.theta())
+
+
 def test_waypoints_200_dual_arm_bitwise():
     p = make(dof=14, waypoints=200, K=64)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
