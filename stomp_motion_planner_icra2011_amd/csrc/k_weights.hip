@@ -537,31 +537,46 @@ void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s)
 
 // delta = M u (policy_improvement.cpp:380), theta += 1.0 * delta (covariant_trajectory_policy.cpp:318-323).
 // With u_all (multi-GPU) u is first summed over the all-gathered block partials in block order.
+// One output per lane, so registers allow a deep ring: kUpdateBatch rows per batch, three
+// batches in flight (the chain waits on M's rows, which the rollout launch evicts from L2)
+#ifndef UPDATE_BATCH
+#define UPDATE_BATCH 4
+#endif
+constexpr int kUpdateBatch = UPDATE_BATCH;
+#ifndef UPDATE_XPRE
+#define UPDATE_XPRE false
+#endif
+
 __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
                                                 int nb_total, double* theta, const int* stop)
 {
-    __shared__ double us[256 + kBandBatch];
-    if (stop && *stop) return;
+    __shared__ double us[256 + 2 * kUpdateBatch];
     const int d = blockIdx.x, i = threadIdx.x;
-    if (i < kBandBatch) us[N + i] = 0.0;
+    // everything independent is issued up front: the stop flag (checked at the store), this
+    // lane's u entry, then (inside band_tile) the first M rows; the LDS fill and its barrier
+    // run while those rows are in flight
+    const int stopped = stop ? *stop : 0;
     const size_t JN = (size_t)J * N;
+    double uv = 0.0;
     if (i < N) {
         if (u_all) {
-            double s = 0.0;
-            for (int b = 0; b < nb_total; ++b) s += u_all[(size_t)b * JN + (size_t)d * N + i];
-            us[i] = s;
+            for (int b = 0; b < nb_total; ++b) uv += u_all[(size_t)b * JN + (size_t)d * N + i];
         } else {
-            us[i] = u[(size_t)d * N + i];
+            uv = u[(size_t)d * N + i];
         }
     }
-    __syncthreads();
+    auto fill = [&]() {
+        if (i < N) us[i] = uv;
+        if (i < 2 * kUpdateBatch) us[N + i] = 0.0;
+        __syncthreads();
+    };
     // k ascending, the noise phase's pinned buffer-load ring (M^T has kMatPadRows zero rows,
-    // us has kBandBatch zero rows past N); whole waves run it, lanes past N store nothing
+    // us has 2 kUpdateBatch zero rows past N: the next batch's rows are read ahead); whole waves run it, lanes past N store nothing
     int col[1] = {min(i, N - 1)};
     double acc[1][1] = {{0.0}};
-    band_tile<1, 0, 1>(MT, N, col, 0, N, us, 1, acc);
+    band_tile<1, 0, 1, kUpdateBatch, decltype(fill), UPDATE_XPRE>(MT, N, col, 0, N, us, 1, acc, fill);
     const double s = acc[0][0];
-    if (i >= N) return;
+    if (i >= N || stopped) return;
     theta[(size_t)d * N + i] += 1.0 * s;
 }
 

@@ -76,11 +76,20 @@ __device__ __forceinline__ void band_product(const double* __restrict__ AT, int 
 constexpr int kBandK = BAND_K;   // rows per batch
 static_assert(kMatPadRows >= 4 * 4 * kBandK && kBandBatch >= kBandK, "band_tile padding");
 constexpr int kCtlRun = 4;  // padded indices per lane in the rollout kernel's control stencils
-template <int TI, int T0, int RT>
+// B rows per batch (default kBandK); loads reach row kend + 4B - 1 and v row kend + B - 1.
+// `mid` runs after the first three batches are issued (k_update fills v there, so its own loads
+// and barrier overlap the ring's first loads).
+struct NoMid {
+    __device__ void operator()() const {}
+};
+// XPRE: v's rows for the next batch are read while this batch sums (v then needs 2B zero
+// rows past kend)
+template <int TI, int T0, int RT, int B = kBandK, class Mid = NoMid, bool XPRE = false>
 __device__ __forceinline__ void band_tile(const double* __restrict__ AT, int N, const int* col, int kbeg, int kend,
-                                          const double* v, int vstride, double (*acc)[RT])
+                                          const double* v, int vstride, double (*acc)[RT], Mid mid = Mid())
 {
-    constexpr int B = kBandK, NT = TI - T0;
+    static_assert(kMatPadRows >= 4 * B, "band_tile look-ahead past the zero rows");
+    constexpr int NT = TI - T0;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)AT, 0, (int)((size_t)(N + kMatPadRows) * N * sizeof(double)), 0x00020000);
     int ioff[NT];
@@ -96,12 +105,23 @@ __device__ __forceinline__ void band_tile(const double* __restrict__ AT, int N, 
                                                            rsrc, ioff[t], (k0 + q) * N * (int)sizeof(double), 0));
         __builtin_amdgcn_sched_barrier(0);   // keep the batch where it is issued
     };
+    double xn[B][RT];
     auto sum = [&](const double (*buf)[NT], int k0) {
         double x[B][RT];
+        if constexpr (XPRE) {
 #pragma unroll
-        for (int q = 0; q < B; ++q)
+            for (int q = 0; q < B; ++q)
 #pragma unroll
-            for (int rr = 0; rr < RT; ++rr) x[q][rr] = v[(k0 + q) * vstride + rr];
+                for (int rr = 0; rr < RT; ++rr) {
+                    x[q][rr] = xn[q][rr];
+                    xn[q][rr] = v[(k0 + B + q) * vstride + rr];
+                }
+        } else {
+#pragma unroll
+            for (int q = 0; q < B; ++q)
+#pragma unroll
+                for (int rr = 0; rr < RT; ++rr) x[q][rr] = v[(k0 + q) * vstride + rr];
+        }
 #pragma unroll
         for (int q = 0; q < B; ++q)
 #pragma unroll
@@ -114,6 +134,13 @@ __device__ __forceinline__ void band_tile(const double* __restrict__ AT, int N, 
     load(A0, k0);
     load(A1, k0 + B);
     load(A2, k0 + 2 * B);
+    mid();
+    if constexpr (XPRE) {
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+#pragma unroll
+            for (int rr = 0; rr < RT; ++rr) xn[q][rr] = v[(kbeg + q) * vstride + rr];
+    }
     for (; b + 4 <= nb; b += 4, k0 += 4 * B) {
         load(A3, k0 + 3 * B); sum(A0, k0);
         load(A0, k0 + 4 * B); sum(A1, k0 + B);
