@@ -334,6 +334,7 @@ class DeviceBuffer:
     """Engine-runtime device allocation (keeps torch's bundled HIP runtime out of the process)."""
 
     def __init__(self, nbytes: int, device: int = 0):
+        self.ptr = None   # set before the call that may raise, so __del__ has nothing to free
         p = C.c_void_p()
         _check(load_library().stomp_device_alloc(device, nbytes, C.byref(p)))
         self.ptr, self.nbytes = p.value, nbytes
