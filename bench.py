@@ -1,22 +1,29 @@
 #!/usr/bin/env python3
 """STOMP iterations/sec on MI355X (BASELINE.json metric), one JSON line on rank 0.
 
-Workload (BASELINE.json configs[1], "cfg2"): 7-DOF PR2-like arm, 100 waypoints
-(N = 99 free), K = 512 noisy rollouts per GPU, no reuse, 256^3 fp32 distance
-field of the shelf + pole scene, built on the device.  A step is one
-PolicyImprovementLoop::runSingleIteration equivalent (noise, projection, control
-costs, K rollout executions, probability weighting, update, noiseless rollout),
-enqueued by stomp_engine_run with inputs already resident in HBM.  With --gpus N
-the K dimension is sharded (K = 512 N, weak scaling) and the per-iteration
-reductions run over RCCL inside the engine.
+Workloads (BASELINE.json configs; --workload, default cfg2 = configs[1], the metric's own):
+  cfg2  7-DOF PR2-like arm, 100 waypoints (N = 99 free), K = 512 rollouts, no reuse, 256^3
+        fp32 distance field of the shelf + pole scene built on the device
+  cfg3  7-DOF, 200 waypoints (N = 199), K = 4096, 256^3
+  cfg4  14-DOF two-arm tree, 100 waypoints, K = 1024, 512^3 (the HBM-bound field)
+  cfg5  64 independent problems (7-DOF, 100 wp, K = 128 each, distinct start / goal / seed),
+        one engine and stream per problem, 64 / N problems per GPU, no communication
+A step is one PolicyImprovementLoop::runSingleIteration equivalent (noise, projection, control
+costs, K rollout executions, probability weighting, update, noiseless rollout), enqueued by
+stomp_engine_run with inputs already resident in HBM.  With --gpus N the K rollouts of the
+workload are sharded over the N ranks (K / N per GPU, STRONG scaling: the global iteration is the
+unit of the metric at every N) and the per-iteration exchanges run over RCCL inside the engine;
+value = global iterations per second.  cfg5 runs replicas (problems split over the ranks).
 
 Also reported:
-  roofline      dominant stage (rollout_cost = fused k_rollout: noise generation + Task::execute):
-                algorithmic bytes per launch K_loc N (4 S + 24 J + 8) + N (4 S + 8 J + 8) over its
-                HIP-event duration, from a second pass of the same K steps with events (the value
-                pass has none)
-  cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread)
-                timed on this host on a bounded sample of the same workload
+  roofline      the dominant kernel k_rollout (noise phase + Task::execute of the K_loc noisy
+                rollouts and the deferred noiseless one): achieved = SURVEY.md 8(d) algorithmic
+                bytes per unit (4 S + 16 J + 8) x (K_loc + 1) N units / its HIP-event average
+                duration (second pass of the same K steps with events; the value pass has none);
+                traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
+  cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread) timed on
+                this host on a bounded sample of the same workload; cpu_baseline_all_cores the
+                banded oracle over the host cores this process may use
 """
 from __future__ import annotations
 
@@ -35,71 +42,77 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "STOMP iterations/sec (7-DOF, 100 wp, K=512, 256³ SDF) at 1/2/4/8 GPUs"
 
+# BASELINE.json configs[1..4] (configs[0] is the reference's own CPU case, cfg1)
+WORKLOADS = {
+    "cfg2": dict(dof=7, waypoints=100, rollouts=512, grid=256, problems=1),
+    "cfg3": dict(dof=7, waypoints=200, rollouts=4096, grid=256, problems=1),
+    "cfg4": dict(dof=14, waypoints=100, rollouts=1024, grid=512, problems=1),
+    "cfg5": dict(dof=7, waypoints=100, rollouts=128, grid=256, problems=64),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--rollouts-per-gpu", type=int, default=512)
-    ap.add_argument("--waypoints", type=int, default=100)
-    ap.add_argument("--dof", type=int, default=7)
-    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
+    ap.add_argument("--rollouts", type=int, default=None, help="K of the whole job (default: the workload's)")
+    ap.add_argument("--waypoints", type=int, default=None)
+    ap.add_argument("--dof", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=None)
+    ap.add_argument("--problems", type=int, default=None, help="cfg5: problems of the whole job")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event pass (no roofline)")
-    ap.add_argument("--problems", type=int, default=1,
-                    help="independent planning problems per GPU, one engine and stream each (cfg5 mode)")
     ap.add_argument("--optimize-steps", type=int, default=200,
                     help="also time StompOptimizer::optimize (device-resident loop) for this many iterations (0 = skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WORKLOADS[a.workload]
+    for k, v in w.items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    a.custom = any(getattr(a, k) != v for k, v in w.items())
+    return a
+
+
+def workload_name(args) -> str:
+    return args.workload + (" (modified)" if args.custom else "")
 
 
 def latest_traffic():
-    """HBM bytes per rollout_cost launch from the newest committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per k_rollout launch from the newest committed rocprofv3 PMC summary (cfg2, one
+    GPU), FETCH_SIZE with and without the gfx950 x2 correction."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*rollout_cost_traffic*.json")))
     if not files:
-        return None
+        return None, None, None
     try:
         with open(files[-1]) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_per_launch_uncorrected"), os.path.basename(files[-1])
     except Exception:
-        return None
+        return None, None, None
 
 
-def cpu_baseline_all_cores(problem, budget_s: float):
-    """SURVEY.md 8(d)'s stronger CPU baseline: the oracle with banded stencils and Task::execute
-    spread over the host cores this process may use (OpenMP over rollouts)."""
-    from oracle import pyoracle as po
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    o = po.Oracle(problem, dense=False, threads=threads)
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        o.iterate(n + 1)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 400:
-            break
-    return {"value": n / el, "unit": "iterations/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} iterations of the same workload on the CPU oracle with banded stencils and "
-                      f"OpenMP over the rollouts' Task::execute, {threads} threads, {el:.1f} s"}
-
-
-def cfg_name(args, world: int) -> str:
-    """The BASELINE.json config a run's shape matches, or "custom"."""
-    shape = (args.dof, args.waypoints, args.rollouts_per_gpu * world, args.grid, args.problems)
-    if shape == (7, 100, 512, 256, 1):
-        return "cfg2"
-    if (args.dof, args.waypoints, args.grid, args.problems) == (7, 200, 256, 1):
-        return "cfg3" if args.rollouts_per_gpu * world == 4096 else "cfg3-shape"
-    if (args.dof, args.waypoints, args.rollouts_per_gpu * world, args.grid, args.problems) == (14, 100, 1024, 512, 1):
-        return "cfg4"
-    if (args.dof, args.waypoints, args.rollouts_per_gpu, args.grid) == (7, 100, 128, 256) and args.problems > 1:
-        return "cfg5"
-    return "custom"
+def host_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"nproc": os.cpu_count(), "sched_affinity": avail, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "model": model}
 
 
 def cpu_baseline(problem, budget_s: float):
+    """SURVEY.md 8(d) CPU baseline: the oracle in reference structure (dense N x N products,
+    sequential per-rollout Task::execute), 1 thread, bounded sample of the same workload."""
     from oracle import pyoracle as po
     o = po.Oracle(problem, dense=True, threads=1)
     t0 = time.perf_counter()
@@ -110,31 +123,62 @@ def cpu_baseline(problem, budget_s: float):
         el = time.perf_counter() - t0
         if el >= budget_s or n >= 200:
             break
-    return {"value": n / el, "unit": "iterations/s", "cores": 1, "kind": "port",
+    return {"value": n / el, "unit": "iterations/s", "cores": 1, "kind": "port", "host": host_info(),
             "sample": f"first {n} iterations of the same workload (K={problem.params.num_rollouts}, N={problem.N}, "
                       f"J={problem.J}, {problem.grid.n}^3 SDF) on the CPU oracle in reference structure "
                       f"(dense N x N products, sequential Task::execute), 1 thread, {el:.1f} s"}
 
 
+def cpu_baseline_all_cores(problem, budget_s: float):
+    """SURVEY.md 8(d)'s stronger CPU baseline: the oracle with banded stencils and Task::execute
+    spread over the host cores this process may use (OpenMP over rollouts)."""
+    from oracle import pyoracle as po
+    threads = int(os.environ.get("OMP_NUM_THREADS") or host_info()["sched_affinity"] or 1)
+    o = po.Oracle(problem, dense=False, threads=threads)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        o.iterate(n + 1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 400:
+            break
+    return {"value": n / el, "unit": "iterations/s", "cores": threads, "kind": "port", "host": host_info(),
+            "sample": f"first {n} iterations of the same workload on the CPU oracle with banded stencils and "
+                      f"OpenMP over the rollouts' Task::execute, {threads} threads, {el:.1f} s"}
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if not dist:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def bench_problems(args, world, rank, local_rank, dist):
-    """cfg5: independent planning problems per GPU (distinct start / goal / seed, one shared
-    device-built SDF), one engine and one stream each, no communication (replicas); each
-    engine's steps are enqueued as one run and the streams run concurrently.  value =
-    problem-iterations per second over all ranks."""
+    """cfg5: the batch of independent planning problems split over the ranks (replicas, no
+    communication), distinct start / goal / seed, one shared device-built SDF per GPU, one engine
+    and one stream each; each engine's steps are enqueued as one run and the streams run
+    concurrently.  value = problem-iterations per second over all ranks."""
     from stomp_motion_planner_icra2011_amd import engine as eng
     from stomp_motion_planner_icra2011_amd import problem as pb
-    P = args.problems
-    rng = np.random.default_rng(1234 + rank)
-    base = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=args.rollouts_per_gpu,
+    P_all = args.problems
+    per = [P_all // world + (1 if r < P_all % world else 0) for r in range(world)]
+    P, first_id = per[rank], sum(per[:rank])
+    rng = np.random.default_rng(1234)
+    base = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=args.rollouts,
                            num_reused_rollouts=0, build_grid=False)
     sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
     eng.sdf_build_device(base, sdf.ptr)
     engines = []
-    for i in range(P):
-        d = rng.uniform(-0.15, 0.15, (2, base.J))
+    offsets = rng.uniform(-0.15, 0.15, (P_all, 2, base.J))
+    for i in range(first_id, first_id + P):
+        d = offsets[i]
         p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid,
-                            num_rollouts=args.rollouts_per_gpu, num_reused_rollouts=0, build_grid=False,
-                            seed=base.seed + 1 + rank * P + i, start=list(base.start + d[0]), goal=list(base.goal + d[1]),
+                            num_rollouts=args.rollouts, num_reused_rollouts=0, build_grid=False,
+                            seed=base.seed + 1 + i, start=list(base.start + d[0]), goal=list(base.goal + d[1]),
                             max_iterations=args.warmup + args.steps + 1)
         engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr))
 
@@ -154,22 +198,22 @@ def bench_problems(args, world, rank, local_rank, dist):
     sweep(args.warmup + 1, args.steps)
     elapsed = time.perf_counter() - t0
     if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    value = P * world * args.steps / elapsed
+        dist.barrier()
+    elapsed = max_over_ranks(dist, elapsed)
+    value = P_all * args.steps / elapsed
     if rank == 0:
         print(json.dumps({
             "metric": "STOMP problem-iterations/sec (64-problem batch, cfg5)", "value": round(value, 3),
             "unit": "problem-iterations/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 5), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 5), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (PR2-like arm, shelf+pole scene, device-built SDF; Philox noise)",
-            "config": {"workload": f"{cfg_name(args, world)}: {P} problems/GPU x {world} GPU, {args.dof}-DOF, {args.waypoints} wp, "
-                                   f"K={args.rollouts_per_gpu} each, {args.grid}^3 SDF shared",
-                       "problems_per_gpu": P, "parallelism": f"replicas x{world}, one stream per problem",
-                       "rollouts_per_s": round(value * args.rollouts_per_gpu, 1)}}))
+            "config": {"workload": f"{workload_name(args)}: {P_all} problems over {world} GPU ({max(per)} per GPU), "
+                                   f"{args.dof}-DOF, {args.waypoints} wp, K={args.rollouts} each, "
+                                   f"{args.grid}^3 SDF shared per GPU",
+                       "problems": P_all, "parallelism": f"replicas x{world}, one stream per problem",
+                       "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "rollouts_per_s": round(value * args.rollouts, 1)}}))
     for e in engines:
         e.close()
     sdf.free()
@@ -177,18 +221,20 @@ def bench_problems(args, world, rank, local_rank, dist):
 
 def main():
     args = parse()
-    if args.problems > 1:
-        # one stream per problem: give HIP as many hardware queues as it needs to run them side by
-        # side (its default, 4, puts several problems' launches in one in-order queue; measured
-        # 24.9k -> 36.4k problem-iterations/s at 8 problems).  Set before the runtime initialises.
-        want = min(32, max(4, 2 * args.problems))
-        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want:
-            os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    if args.workload == "cfg5":
+        # one stream per problem: give HIP as many hardware queues as it can use to run them
+        # side by side (its default, 4, puts several problems' launches in one in-order queue;
+        # measured 24.9k -> 36.4k problem-iterations/s at 8 problems).  Set before the runtime
+        # initialises.
+        per_gpu = (args.problems + world - 1) // world
+        want = min(32, max(4, 2 * per_gpu))
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     dist = None
     if world > 1:
         import torch.distributed as dist  # CPU rendezvous only: the data path is RCCL inside the engine
@@ -197,13 +243,15 @@ def main():
     from stomp_motion_planner_icra2011_amd import engine as eng
     from stomp_motion_planner_icra2011_amd import problem as pb
 
-    if args.problems > 1:
+    if args.workload == "cfg5":
         bench_problems(args, world, rank, local_rank, dist)
         if dist:
             dist.destroy_process_group()
         return
 
-    K = args.rollouts_per_gpu * world
+    K = args.rollouts
+    if K % (64 * world) != 0:
+        raise SystemExit(f"K={K} must split into whole 64-rollout blocks over {world} GPUs")
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
                         num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + 2 * args.steps + 1)
     sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
@@ -227,18 +275,9 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, t1 - t0)
     ms_per_step = 1000.0 * elapsed / args.steps
-    global_its = args.steps / elapsed
-    # The metric's unit is a K = 512 iteration (BASELINE.json).  With K = 512 per GPU the N-GPU
-    # run does one K = 512 N iteration per step, i.e. N units of the metric's work, so the
-    # whole-job aggregate is N x the global iteration rate (at N = 1 the two are the same).
-    value = global_its * world
+    value = args.steps / elapsed   # global iterations (of the whole K) per second
 
     # Kernel durations: the same K steps again with HIP events recorded around every stage
     # on the engine stream.  The events themselves cost ~10 us of dispatch gap per stage,
@@ -255,42 +294,48 @@ def main():
 
     S = len(p.spheres)
     K_loc = e.K_loc
-    # each launch generates and evaluates K_loc noisy rollouts (noise, params and control rows
-    # written: 24 J N bytes; SDF gathers 4 S N; state costs 8 N) and evaluates the deferred
-    # noiseless rollout of theta (reads 8 J N)
-    bytes_per_launch = K_loc * p.N * (4 * S + 24 * p.J + 8) + p.N * (4 * S + 8 * p.J + 8)
+    # per (rollout, waypoint) unit, one fp32 SDF voxel per sphere (4 S), the
+    # write + read of the fp64 noise per joint (16 J) and the fp64 state cost (8); one k_rollout
+    # launch executes the K_loc noisy rollouts of this rank and the deferred noiseless one
+    unit_bytes = 4 * S + 16 * p.J + 8
+    bytes_per_launch = (K_loc + 1) * p.N * unit_bytes
+    # the same launch counting every row it writes (noise, params, control: 24 J) and the
+    # noiseless rollout's params read (8 J) instead of 16 J
+    bytes_written_rows = K_loc * p.N * (4 * S + 24 * p.J + 8) + p.N * (4 * S + 8 * p.J + 8)
     roofline = None
     if timing.get("rollout_cost", {}).get("launches"):
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
         achieved = bytes_per_launch / avg_s / 1e9
+        traffic, traffic_raw, traffic_src = latest_traffic()
+        headline = args.workload == "cfg2" and not args.custom and world == 1
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "frac": round(achieved / HBM_PEAK_GBS, 5),
                     # the committed PMC summary is of the default workload (cfg2, one GPU)
-                    "traffic": latest_traffic() if cfg_name(args, world) == "cfg2" else None,
-                    "kernel": "rollout_cost (k_rollout)", "bytes_per_launch": bytes_per_launch,
-                    "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3)}
-    if roofline is not None:
-        # whole iteration, B_iter = E * N * (4 S + 16 J + 8), E = K + 1, all ranks
-        b_iter = (K + 1) * p.N * (4 * S + 16 * p.J + 8)
-        roofline["iteration_bytes"] = b_iter
-        roofline["iteration_frac"] = round(b_iter * global_its / (HBM_PEAK_GBS * 1e9 * world), 5)   # vs N x peak
+                    "traffic": traffic if headline else None,
+                    "traffic_uncorrected": traffic_raw if headline else None,
+                    "traffic_source": traffic_src if headline else None,
+                    "kernel": "k_rollout", "unit_bytes": unit_bytes, "units_per_launch": (K_loc + 1) * p.N,
+                    "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3),
+                    "frac_vs_measured_6290": round(achieved / 6290.0, 5),
+                    "sdf_only_gbs": round((K_loc + 1) * p.N * 4 * S / avg_s / 1e9, 2),
+                    "frac_rows_written_24J": round(bytes_written_rows / avg_s / 1e9 / HBM_PEAK_GBS, 5),
+                    "iteration_bytes": (K + 1) * p.N * unit_bytes,
+                    "iteration_frac": round((K + 1) * p.N * unit_bytes * value / (HBM_PEAK_GBS * 1e9 * world), 5)}
 
     # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
     # the same iterations with the optimizer's bookkeeping, no early stop
     optimize = None
-    if args.optimize_steps > 0:
+    if args.optimize_steps > 0 and world == 1:
         po_ = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
                               num_reused_rollouts=0, build_grid=False, max_iterations=args.optimize_steps,
                               max_iterations_after_collision_free=args.optimize_steps + 1)
-        eo = eng.Engine(po_, device=local_rank, sdf_device_ptr=sdf.ptr, rank=rank, world_size=world, comm_id=comm_id) \
-            if world == 1 else None
-        if eo is not None:
-            eo.optimize()   # warm
-            t0 = time.perf_counter()
-            st, _ = eo.optimize()
-            dt = time.perf_counter() - t0
-            optimize = {"iterations": st.iterations, "iterations_per_s": round(st.iterations / dt, 3)}
-            eo.close()
+        eo = eng.Engine(po_, device=local_rank, sdf_device_ptr=sdf.ptr)
+        eo.optimize()   # warm
+        t0 = time.perf_counter()
+        st, _ = eo.optimize()
+        dt = time.perf_counter() - t0
+        optimize = {"iterations": st.iterations, "iterations_per_s": round(st.iterations / dt, 3)}
+        eo.close()
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -303,16 +348,13 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "iterations/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (PR2-like arm, shelf+pole scene, device-built SDF; Philox noise)",
-            "config": {"workload": f"{cfg_name(args, world)}: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={args.rollouts_per_gpu}/GPU "
-                                   f"(K={K} total), K_r=0, {args.grid}^3 SDF, S={S} spheres",
-                       "rollouts_per_gpu": args.rollouts_per_gpu, "global_rollouts": K,
+            "config": {"workload": f"{workload_name(args)}: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={K} "
+                                   f"({K_loc}/GPU), K_r=0, {args.grid}^3 SDF, S={S} spheres",
+                       "global_rollouts": K, "rollouts_per_gpu": K_loc,
                        "parallelism": f"rollout shard x{world}" + (" (RCCL)" if world > 1 else ""),
-                       "global_iterations_per_s": round(global_its, 3),
-                       "value_unit": f"iterations of K={args.rollouts_per_gpu} per second, summed over GPUs "
-                                     f"(= global K={K} iterations/s x {world})",
-                       "rollouts_per_s": round(global_its * K, 1)},
+                       "rollouts_per_s": round(value * K, 1)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_mt,

@@ -199,8 +199,10 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* stats, double* costs_per
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj);
 int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
 
-/* Inspection for parity tests.  which: "params","noise","noise_projected"(if kept),
- * "control_costs","probabilities" -> K_local x J x N; "state_costs" -> K_local x N. */
+/* Inspection for parity tests.  which: "params","noise","control_costs","probabilities"
+ * -> K_local x J x N; "state_costs" -> K_local x N; the extra (noiseless) rollout of
+ * addExtraRollouts (policy_improvement.cpp:443-462): "x_params","x_noise","x_control_costs"
+ * -> J x N (kept with K_r > 0 only), "x_state_costs" -> N. */
 int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out);
 /* which: "Rinv","L","M","Qinv" (N x N, joint selects Qinv), "R" (free block of the
  * control-cost matrix, CovariantTrajectoryPolicy::getControlCosts,
@@ -224,6 +226,10 @@ int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
 int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
                     double max_expansion, const double* boxes, int32_t n_boxes, const double* cylinders,
                     int32_t n_cylinders, float* out_device, void* stream);
+
+/* The differentiation stencils the engine is built on (DIFF_RULES of stomp_utils.h:49-56:
+ * velocity, acceleration, jerk; 3 x 7 doubles, row-major).  Host only, no device needed. */
+int stomp_diff_rules(double* out);
 
 /* Device buffers for callers without a HIP runtime of their own (bench, tests). */
 int stomp_device_alloc(int32_t device, uint64_t bytes, void** out);

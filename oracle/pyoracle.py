@@ -58,7 +58,7 @@ class so_config(C.Structure):
                 ("sum_block", C.c_int), ("dense", C.c_int), ("threads", C.c_int),
                 ("inertias", C.POINTER(so_inertia)), ("torque_root", C.c_int), ("torque_tip", C.c_int),
                 ("gravity", C.c_double * 3), ("num_orientation_constraints", C.c_int),
-                ("orientation_constraints", C.POINTER(so_orientation_constraint))]
+                ("orientation_constraints", C.POINTER(so_orientation_constraint)), ("ref_arith", C.c_int)]
 
 
 class so_iter_out(C.Structure):
@@ -98,6 +98,7 @@ def lib():
         l.so_get_rollouts.argtypes = [P, C.c_char_p, dp]
         l.so_philox4x32.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         l.so_normals.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, dp]
+        l.so_diff_rules.argtypes = [dp]
         l.so_exp.restype = C.c_double
         l.so_exp.argtypes = [C.c_double]
         l.so_log.restype = C.c_double
@@ -128,7 +129,10 @@ def _arr(vals, T):
 class Oracle:
     """One planning problem on the CPU oracle (keeps every buffer it points at alive)."""
 
-    def __init__(self, problem, dense: bool = False, threads: int = 1, sum_block: int = 64):
+    def __init__(self, problem, dense: bool = False, threads: int = 1, sum_block: int = 64, ref_arith: bool = False):
+        """dense: the reference's dense N x N products (CPU baseline structure); ref_arith: the
+        reference's written arithmetic order (non-fused L z / M eps, sequential rollout sums)
+        instead of the engine's contract."""
         L = lib()
         p = problem
         self.problem = p
@@ -191,6 +195,7 @@ class Oracle:
                          for c in p.orientation_constraints], so_orientation_constraint)
         cfg.num_orientation_constraints = len(p.orientation_constraints)
         cfg.orientation_constraints = self._oc
+        cfg.ref_arith = int(ref_arith)
         self._cfg = cfg
         self.h = L.so_create(C.byref(cfg))
         if not self.h:
@@ -255,7 +260,10 @@ class Oracle:
         return out
 
     def rollouts(self, which: str) -> np.ndarray:
-        shape = (self.K, self.N) if which == "state_costs" else (self.K, self.J, self.N)
+        if which.startswith("x_"):
+            shape = (self.N,) if which == "x_state_costs" else (self.J, self.N)
+        else:
+            shape = (self.K, self.N) if which == "state_costs" else (self.K, self.J, self.N)
         out = np.zeros(shape)
         if lib().so_get_rollouts(self.h, which.encode(), _dp(out)) != 0:
             raise KeyError(which)
@@ -296,6 +304,12 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().so_philox4x32(c, k, o)
     return list(o)
+
+
+def diff_rules() -> np.ndarray:
+    out = np.zeros((3, 7))
+    lib().so_diff_rules(_dp(out))
+    return out
 
 
 def dexp(x: float) -> float:

@@ -12,6 +12,13 @@
  * sequentially from 0.0, block partials then summed sequentially from 0.0);
  * for K <= sum_block this is exactly the reference's sequential order
  * (policy_improvement.cpp:352-358, 376-379).
+ *
+ * cfg.ref_arith = 1 drops the two engine-contract choices and follows the reference's
+ * written order everywhere: L z and M eps non-fused and k ascending over the dense matrix
+ * (multivariate_gaussian.h:93, policy_improvement.cpp:477), and the rollout sums of P and
+ * eps * P sequential over all K (policy_improvement.cpp:352-358, 376-379).
+ * tests/test_reference_order.py measures how far the engine contract drifts from it on the
+ * north-star quantity (best_group_trajectory_).
  */
 #include "stomp_oracle.h"
 #include "dmath.h"
@@ -183,6 +190,7 @@ void so_normals(uint64_t seed, int iteration, int joint, int rollout, int n, dou
     }
 }
 
+void so_diff_rules(double* out) { memcpy(out, DIFF_RULES, sizeof DIFF_RULES); }
 double so_exp(double x) { return dm_exp(x); }
 double so_log(double x) { return dm_log(x); }
 void so_sincos(double x, double* s, double* c) { dm_sincos(x, s, c); }
@@ -716,6 +724,7 @@ so_problem* so_create(const so_config* cfg)
     P->S = cfg->num_spheres;
     P->nseg = cfg->num_segments;
     P->B = cfg->sum_block > 0 ? cfg->sum_block : 64;
+    if (cfg->ref_arith) P->B = cfg->num_rollouts;   /* one block: the reference's sequential sums */
     P->cfg.noise_stddev = dup_d(cfg->noise_stddev, J);
     P->cfg.noise_decay = dup_d(cfg->noise_decay, J);
     P->cfg.start = dup_d(cfg->start, J);
@@ -1192,6 +1201,18 @@ static void matvec_fma(const double* A, int n, const double* x, double* y, int l
     }
 }
 
+static void matvec(const double* A, int n, const double* x, double* y, int lower_only);
+
+/* the noise path's products under the configured contract: the engine's fma chain, or
+ * (ref_arith) the reference's written order -- dense, k ascending, one rounding per multiply
+ * and per add (Eigen 2's MatrixXd * VectorXd under SSE2 without FMA, CMakeLists.txt:34; its
+ * internal blocking is third-party and not restated, parity unpinned there) */
+static void noise_product(const so_problem* P, const double* A, int n, const double* x, double* y, int lower_only)
+{
+    if (P->cfg.ref_arith) matvec(A, n, x, y, 0);
+    else matvec_fma(A, n, x, y, lower_only);
+}
+
 static void matvec(const double* A, int n, const double* x, double* y, int lower_only)
 {
     for (int i = 0; i < n; ++i) {
@@ -1308,7 +1329,7 @@ static void generate_rollouts(so_problem* P, int iteration_number, const double*
             const int d = dr / K_gen, r = dr % K_gen;
             so_normals(P->cfg.seed, iteration_number, d, r, N, z);
             /* MultivariateGaussian::sample: output = mean + L * z (multivariate_gaussian.h:88-94) */
-            matvec_fma(P->L, N, z, tmp, !P->cfg.dense);
+            noise_product(P, P->L, N, z, tmp, !P->cfg.dense);
             double* nz = P->r_noise + r * JN + (size_t)d * N;
             double* pr = P->r_params + r * JN + (size_t)d * N;
             for (int t = 0; t < N; ++t) {
@@ -1352,7 +1373,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
 #endif
     for (int r = 0; r < K; ++r)
         for (int d = 0; d < J; ++d)
-            matvec_fma(P->M, N, P->r_noise + r * JN + (size_t)d * N, P->r_nproj + r * JN + (size_t)d * N, 0);
+            noise_product(P, P->M, N, P->r_noise + r * JN + (size_t)d * N, P->r_nproj + r * JN + (size_t)d * N, 0);
 
     /* Task::execute for each generated rollout (policy_improvement_loop.cpp:165-170) */
 #ifdef _OPENMP
@@ -1436,7 +1457,7 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
         /* addExtraRollouts (policy_improvement.cpp:443-462) */
         memcpy(P->x_params, P->theta, JN * 8);
         for (size_t k = 0; k < JN; ++k) P->x_noise[k] = P->x_params[k] - P->theta[k];
-        for (int d = 0; d < J; ++d) matvec_fma(P->M, N, P->x_noise + (size_t)d * N, P->x_nproj + (size_t)d * N, 0);
+        for (int d = 0; d < J; ++d) noise_product(P, P->M, N, P->x_noise + (size_t)d * N, P->x_nproj + (size_t)d * N, 0);
         double* xall = dalloc((size_t)Nall);
         double* call = dalloc((size_t)Nall);
         control_costs(P, P->x_params, P->x_nproj, 0.5 * P->cfg.smoothness_cost_weight, P->x_ctrl, xall, call);
@@ -1518,6 +1539,11 @@ int so_get_rollouts(const so_problem* P, const char* which, double* out)
     else if (!strcmp(which, "control_costs")) memcpy(out, P->r_ctrl, KJN * 8);
     else if (!strcmp(which, "probabilities")) memcpy(out, P->r_prob, KJN * 8);
     else if (!strcmp(which, "state_costs")) memcpy(out, P->r_state, (size_t)P->K * P->N * 8);
+    else if (!strcmp(which, "x_params")) memcpy(out, P->x_params, (size_t)P->J * P->N * 8);
+    else if (!strcmp(which, "x_noise")) memcpy(out, P->x_noise, (size_t)P->J * P->N * 8);
+    else if (!strcmp(which, "x_noise_projected")) memcpy(out, P->x_nproj, (size_t)P->J * P->N * 8);
+    else if (!strcmp(which, "x_control_costs")) memcpy(out, P->x_ctrl, (size_t)P->J * P->N * 8);
+    else if (!strcmp(which, "x_state_costs")) memcpy(out, P->x_state, (size_t)P->N * 8);
     else { set_err("unknown rollout field"); return -1; }
     return 0;
 }

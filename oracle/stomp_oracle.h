@@ -124,6 +124,9 @@ typedef struct {
     /* path constraints (stomp_optimizer.cpp:195-201, 1107-1115) */
     int num_orientation_constraints;
     const so_orientation_constraint* orientation_constraints;
+    /* 1: the reference's written arithmetic order: non-fused dense L z / M eps and sequential
+     * rollout sums over all K (instead of the engine's fma chain and 64-rollout blocks) */
+    int ref_arith;
 } so_config;
 
 typedef struct so_problem so_problem;
@@ -174,12 +177,14 @@ int so_get_last_trajectory(const so_problem* p, double* traj /* J x N */);
 
 /* rollout state after so_iterate, for stage tests. which:
  * "params","noise","noise_projected","control_costs","probabilities" -> K x J x N;
- * "state_costs" -> K x N */
+ * "state_costs" -> K x N; the extra rollout (addExtraRollouts): "x_params","x_noise",
+ * "x_noise_projected","x_control_costs" -> J x N, "x_state_costs" -> N */
 int so_get_rollouts(const so_problem* p, const char* which, double* out);
 
 /* stage primitives */
 void so_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 void so_normals(uint64_t seed, int iteration, int joint, int rollout, int n, double* z);
+void so_diff_rules(double* out /* 3 x 7: DIFF_RULES, stomp_utils.h:49-56 */);
 double so_exp(double x);
 double so_log(double x);
 void so_sincos(double x, double* s, double* c);

@@ -135,6 +135,21 @@ int fail(stomp_engine* e, int code, const char* fmt, ...)
     return code;
 }
 
+// Every C-ABI entry on an engine runs with the engine's device current (allocations, launches
+// and attribute opt-ins land there) and restores the caller's device on return.
+struct DeviceGuard {
+    int prev = -1, dev;
+    explicit DeviceGuard(int d) : dev(d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+
 #define HIP_TRY(e, x)                                                                          \
     do {                                                                                       \
         hipError_t _st = (x);                                                                  \
@@ -567,9 +582,15 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         launch_noiseless(e, member);
     }
     if (e->Kr > 0) {
-        // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0
-        hipMemcpyAsync(e->d_x_params, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToDevice, e->stream);
+        // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0.  Not
+        // gated by the optimize loop's stop flag: the reference prices the extra rollout before
+        // it breaks (stomp_optimizer.cpp:293 -> policy_improvement_loop.cpp:192), and the next
+        // iteration's reuse ranking reads it.  After a stop theta no longer changes, so the
+        // launches of iterations enqueued past it recompute the same row.
+        HIP_TRY(e, hipMemcpyAsync(e->d_x_params, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToDevice,
+                                  e->stream));
         NoiseArgs xa = na;
+        xa.stop = nullptr;
         xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 1; xa.row_begin = 0;
         xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
         launch_noise(xa, e->stream);
@@ -625,6 +646,9 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     const int world = d->world_size > 0 ? d->world_size : 1;
     if (world > 1) {
+        if (!d->comm_id) return fail(nullptr, STOMP_E_INVALID, "world_size > 1 needs a comm_id");
+        if (d->rank < 0 || d->rank >= world)
+            return fail(nullptr, STOMP_E_INVALID, "rank %d outside [0, world_size %d)", d->rank, world);
         if (d->num_reused_rollouts > 0)
             return fail(nullptr, STOMP_E_UNSUPPORTED, "rollout reuse is single-device only");
         if (d->num_rollouts % (world * kSumBlock) != 0)
@@ -634,6 +658,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
 #endif
     }
 
+    DeviceGuard dg(d->device);
     stomp_engine* e = new stomp_engine();
     e->device = d->device;
     int rc;
@@ -983,12 +1008,16 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
 
 void stomp_engine_destroy(stomp_engine* e)
 {
+    if (!e) return;
+    DeviceGuard dg(e->device);
     release(e);
     delete e;
 }
 
 int stomp_engine_get_theta(stomp_engine* e, double* theta)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     HIP_TRY(e, hipMemcpyAsync(theta, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
@@ -996,6 +1025,8 @@ int stomp_engine_get_theta(stomp_engine* e, double* theta)
 
 int stomp_engine_set_theta(stomp_engine* e, const double* theta)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);   // a pending noiseless rollout belongs to the theta being replaced
     HIP_TRY(e, hipMemcpyAsync(e->d_theta, theta, sizeof(double) * e->J * e->N, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -1004,6 +1035,8 @@ int stomp_engine_set_theta(stomp_engine* e, const double* theta)
 
 int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);
     int rc = enqueue_iteration(e, it, false);
     if (rc) return rc;
@@ -1021,6 +1054,8 @@ int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
 
 int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     // the last iteration's noiseless rollout stays pending: it rides in the next rollout
     // launch, or is flushed by synchronize, iterate, set_theta and the trajectory reads
     for (int i = 0; i < count; ++i) {
@@ -1032,6 +1067,8 @@ int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count)
 
 int stomp_engine_synchronize(stomp_engine* e)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
@@ -1040,6 +1077,8 @@ int stomp_engine_synchronize(stomp_engine* e)
 int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double* costs, uint8_t* collision_free,
                       double* traj_out, int32_t iteration_member, uint8_t* constraints_satisfied)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     if (num <= 0) return 0;
     const size_t JN = (size_t)e->J * e->N;
     if (num > e->eval_cap) {
@@ -1084,6 +1123,8 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
 // never waits on the host.
 int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);
     DevTrack init{};
     init.stop = 0; init.cfi = 0; init.iterations = 0; init.success = 0;
@@ -1160,6 +1201,8 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
 
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_best_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -1168,6 +1211,8 @@ int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
 
 int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_last_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -1176,6 +1221,8 @@ int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj)
 
 int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     const size_t KJN = (size_t)e->K_loc * e->J * e->N;
     const double* src = nullptr;
     size_t n = KJN;
@@ -1184,6 +1231,17 @@ int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
     else if (!std::strcmp(which, "control_costs")) src = e->d_control;
     else if (!std::strcmp(which, "probabilities")) src = e->d_prob;
     else if (!std::strcmp(which, "state_costs")) { src = e->d_state; n = (size_t)e->K_loc * e->N; }
+    else if (!std::strncmp(which, "x_", 2)) {
+        // the extra (noiseless) rollout of addExtraRollouts (policy_improvement.cpp:443-462);
+        // x_state_costs is written by every noiseless rollout, the others only with reuse
+        flush_noiseless(e);
+        n = (size_t)e->J * e->N;
+        if (!std::strcmp(which, "x_params")) src = e->d_x_params;
+        else if (!std::strcmp(which, "x_noise")) src = e->d_x_noise;
+        else if (!std::strcmp(which, "x_control_costs")) src = e->d_x_control;
+        else if (!std::strcmp(which, "x_state_costs")) { src = e->d_x_state; n = (size_t)e->N; }
+        else return fail(e, STOMP_E_INVALID, "unknown rollout field '%s'", which);
+    }
     else return fail(e, STOMP_E_INVALID, "unknown rollout field '%s'", which);
     HIP_TRY(e, hipMemcpyAsync(out, src, n * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
@@ -1210,6 +1268,8 @@ int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, d
 
 int stomp_engine_get_pad_positions(stomp_engine* e, double* out)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     HIP_TRY(e, hipMemcpyAsync(out, e->d_pad_pos, sizeof(double) * 12 * e->S * 3, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     return 0;
@@ -1217,6 +1277,8 @@ int stomp_engine_get_pad_positions(stomp_engine* e, double* out)
 
 int stomp_engine_set_timing(stomp_engine* e, int32_t enable)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     collect_timing(e);
     e->timing = enable != 0;
     for (int i = 0; i < T_COUNT; ++i) { e->tot_ms[i] = 0; e->launches[i] = 0; }
@@ -1225,6 +1287,8 @@ int stomp_engine_set_timing(stomp_engine* e, int32_t enable)
 
 int stomp_engine_get_timing(stomp_engine* e, const char* name, double* total_ms, int32_t* launches)
 {
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
     collect_timing(e);
     double t = 0;
     int n = 0;
@@ -1318,6 +1382,13 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
     if (d_c) hipFree(d_c);
     if (d_z) hipFree(d_z);
     if (st != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(st));
+    return 0;
+}
+
+int stomp_diff_rules(double* out)
+{
+    if (!out) return fail(nullptr, STOMP_E_INVALID, "null argument");
+    std::memcpy(out, kDiffRules, sizeof(double) * kNumDiffRules * kDiffRuleLength);
     return 0;
 }
 

@@ -524,13 +524,7 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     const int blocks = a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
-    if (lds > 64 * 1024) {
-        static size_t raised = 0;   // opt in to more than the default 64 KB once per size
-        if (lds > raised) {
-            (void)hipFuncSetAttribute((const void*)k_rollout<kBlock>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            raised = lds;
-        }
-    }
+    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock>, lds);
     hipLaunchKernelGGL((k_rollout<kBlock>), dim3(blocks), dim3(kBlock), lds, s, m, a);
 }
 

@@ -2,7 +2,25 @@
 // distance-field construction.
 #include "device_fk.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 namespace stomp {
+
+void lds_opt_in(const void* kernel, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, size_t> raised;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    size_t& r = raised[{kernel, dev}];
+    if (bytes > r) {
+        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        r = bytes;
+    }
+}
 
 // padding-point sphere positions: iteration-0 full FK of start (rows 0..5) and goal (rows 6..11)
 // (stomp_optimizer.cpp:626-630 with JntToCartFull; padding rows of the group trajectory hold

@@ -337,18 +337,10 @@ void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s)
     if (blocks <= 0) return;
     const size_t lds = terms_lds_bytes(m);
     if (m.N <= 128) {
-        static size_t raised = 0;
-        if (lds > 64 * 1024 && lds > raised) {
-            (void)hipFuncSetAttribute((const void*)k_terms<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            raised = lds;
-        }
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_terms<128>, lds);
         hipLaunchKernelGGL((k_terms<128>), dim3(blocks), dim3(128), lds, s, m, a);
     } else {
-        static size_t raised = 0;
-        if (lds > 64 * 1024 && lds > raised) {
-            (void)hipFuncSetAttribute((const void*)k_terms<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            raised = lds;
-        }
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_terms<256>, lds);
         hipLaunchKernelGGL((k_terms<256>), dim3(blocks), dim3(256), lds, s, m, a);
     }
 }

@@ -463,21 +463,11 @@ static void launch_rows(const WeightArgs& a, const NoiseArgs* pre, hipStream_t s
         const RolloutLds L = rollout_lds(pre->J, pre->N, 0, 0, 0, 0, 0, 0, 0);
         const size_t lp = 2 * (size_t)(L.nzB - L.nzA);
         if (lp > lds) lds = lp;
-        static size_t raised_pre = 0;
-        if (lds > 48 * 1024 && lds > raised_pre) {
-            (void)hipFuncSetAttribute((const void*)k_weights_rows_pre<TCW, EPT>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            raised_pre = lds;
-        }
+        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_pre<TCW, EPT>, lds);
         hipLaunchKernelGGL((k_weights_rows_pre<TCW, EPT>), dim3(nw + pre->K_loc), dim3(256), lds, s, a, *pre, nw);
         return;
     }
-    static size_t raised = 0;   // opt in to more than the default 64 KB once per size
-    if (lds > 48 * 1024 && lds > raised) {
-        (void)hipFuncSetAttribute((const void*)k_weights_rows<TCW, EPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        raised = lds;
-    }
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows<TCW, EPT>, lds);
     hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(kWRB), lds, s, a);
 }
 

@@ -233,6 +233,11 @@ struct TermsArgs {
     uint8_t* x_cs;
 };
 
+// hipFuncAttributeMaxDynamicSharedMemorySize opt-in for more than the default dynamic LDS:
+// remembered per (kernel, current device), thread-safe (engines on several devices or host
+// threads share the kernels)
+void lds_opt_in(const void* kernel, size_t bytes);
+
 size_t terms_lds_bytes(const TermsModel& m);
 void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
 

@@ -81,7 +81,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_engine_get_matrix", "stomp_engine_get_pad_positions", "stomp_engine_set_timing",
             "stomp_engine_get_timing", "stomp_engine_local_rollouts", "stomp_sdf_build", "stomp_comm_unique_id",
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
-            "stomp_device_copy_to_host", "stomp_device_count"]
+            "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules"]
 
 _lib = None
 
@@ -126,6 +126,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_device_free.argtypes = [C.c_void_p]
     l.stomp_device_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     l.stomp_device_count.argtypes = [C.POINTER(C.c_int32)]
+    l.stomp_diff_rules.argtypes = [dp]
     l.stomp_device_selftest.argtypes = [dp, C.c_int32, dp, dp, dp, dp, dp]
     l.stomp_device_normals.argtypes = [C.c_uint64, C.c_int32, C.c_int32, C.c_int32, C.c_int32, dp]
     _lib = l
@@ -306,7 +307,10 @@ class Engine:
         return out
 
     def rollouts(self, which: str) -> np.ndarray:
-        shape = (self.K_loc, self.N) if which == "state_costs" else (self.K_loc, self.J, self.N)
+        if which.startswith("x_"):
+            shape = (self.N,) if which == "x_state_costs" else (self.J, self.N)
+        else:
+            shape = (self.K_loc, self.N) if which == "state_costs" else (self.K_loc, self.J, self.N)
         out = np.zeros(shape)
         _check(load_library().stomp_engine_get_rollouts(self.h, which.encode(), _dp(out)), self.h)
         return out
@@ -352,6 +356,13 @@ class DeviceBuffer:
 
     def __del__(self):
         self.free()
+
+
+def diff_rules() -> np.ndarray:
+    """DIFF_RULES as compiled into the engine (host only)."""
+    out = np.zeros((3, 7))
+    _check(load_library().stomp_diff_rules(_dp(out)))
+    return out
 
 
 def device_count() -> int:

@@ -290,7 +290,7 @@ def test_golden_execute_cases():
         np.testing.assert_array_equal(cf, g[f"cf_{dof}"])
 
 
-@pytest.mark.parametrize("K,Kr,after_cf", [(20, 10, 3), (10, 0, 1), (20, 10, 1000)])
+@pytest.mark.parametrize("K,Kr,after_cf", [(20, 10, 3), (10, 0, 1), (20, 10, 1000), (16, 8, 1)])
 def test_device_optimize_loop_stops_like_the_reference(K, Kr, after_cf):
     # the device-resident loop (k_track + stop flag, chunks enqueued ahead) must stop at the
     # reference's iteration (stomp_optimizer.cpp:340-344), leave theta as the last executed
@@ -307,5 +307,10 @@ def test_device_optimize_loop_stops_like_the_reference(K, Kr, after_cf):
     np.testing.assert_array_equal(e.best_trajectory(), o.best_trajectory())
     np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory())
     np.testing.assert_array_equal(e.theta(), o.theta())
+    # the extra (noiseless) rollout the next iteration's reuse ranking reads: priced on the
+    # iteration the loop stops at too (addExtraRollouts runs before the break)
+    fields = ("x_params", "x_noise", "x_control_costs", "x_state_costs") if Kr > 0 else ("x_state_costs",)
+    for f in fields:
+        np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f)
     for it in range(est.iterations + 1, est.iterations + 3):
         _compare_iteration(o, e, it)

@@ -1,0 +1,71 @@
+"""How far the engine's floating-point contract drifts from the reference's written order.
+
+The engine (and the oracle in its default mode, which the GPU matches bit for bit) makes two
+arithmetic choices the reference does not:
+  * L z and M eps as k-ascending fma chains (the fp64 matrix cores), where the reference's
+    Eigen 2 products round every multiply and add (SSE2, CMakeLists.txt:34;
+    multivariate_gaussian.h:93, policy_improvement.cpp:477);
+  * sums over rollouts in fixed 64-rollout blocks, where the reference sums P and eps * P
+    sequentially over all K (policy_improvement.cpp:352-358, 376-379).
+oracle ref_arith=1 follows the reference's written order instead (dense products, non-fused,
+one block).  Both modes share the same normals, so the difference is the arithmetic alone.
+North-star bar: best_group_trajectory_ within 1e-5 (BASELINE.json north_star); the observed
+drift is ~1e-14.  (Eigen 2's internal product blocking is third-party code that is not in
+the container, so its exact order stays unpinned)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from stomp_motion_planner_icra2011_amd import problem as pb
+
+TOL_FINAL = 1e-5
+THREADS = min(8, os.cpu_count() or 1)
+
+
+def optimize_both(p):
+    out = []
+    for ref in (False, True):
+        o = po.Oracle(p, threads=THREADS, dense=ref, ref_arith=ref)
+        st, costs = o.optimize()
+        out.append((st, costs, o.best_trajectory(), o.last_trajectory(), o.theta()))
+    return out
+
+
+@pytest.mark.parametrize("name,kw", [
+    # cfg1 (BASELINE configs[0]): K=20, 10 reused, 128^3, 100 optimize iterations
+    ("cfg1", dict(grid_n=128, num_rollouts=20, num_reused_rollouts=10, max_iterations=100)),
+    # cfg2 (configs[1]): K=512, 256^3, 20 optimize iterations
+    ("cfg2", dict(grid_n=256, num_rollouts=512, num_reused_rollouts=0, max_iterations=20)),
+])
+def test_engine_contract_vs_reference_order(name, kw):
+    p = pb.make_problem(max_iterations_after_collision_free=1000, **kw)
+    (sa, ca, ba, la, ta), (sb, cb, bb, lb, tb) = optimize_both(p)
+    assert sa.iterations == sb.iterations == kw["max_iterations"]
+    # the same decisions: collision-free streaks and best-iteration bookkeeping
+    assert (sa.success, sa.success_iteration, sa.collision_success_iteration, sa.last_improvement_iteration) == \
+        (sb.success, sb.success_iteration, sb.collision_success_iteration, sb.last_improvement_iteration)
+    d_best = np.abs(ba - bb).max()
+    d_last = np.abs(la - lb).max()
+    d_theta = np.abs(ta - tb).max()
+    print(f"{name}: max |best diff| {d_best:.3e}, |last diff| {d_last:.3e}, |theta diff| {d_theta:.3e}, "
+          f"|cost diff| {np.abs(ca - cb).max():.3e}")
+    assert d_best <= TOL_FINAL
+    assert d_last <= TOL_FINAL and d_theta <= TOL_FINAL
+    np.testing.assert_allclose(ca, cb, rtol=1e-9, atol=1e-9)
+    # the modes are genuinely different arithmetic (not the same code path)
+    assert not np.array_equal(ta, tb)
+
+
+def test_sequential_sums_equal_blocked_for_small_K():
+    # K <= 64: one block is the reference's sequential order, so only the fma contract differs
+    p = pb.make_problem(grid_n=64, num_rollouts=10, num_reused_rollouts=5)
+    a = po.Oracle(p, ref_arith=False)
+    b = po.Oracle(p, ref_arith=True, dense=True)
+    for it in range(1, 4):
+        a.iterate(it)
+        b.iterate(it)
+    # identical normals and parameters up to the product rounding
+    np.testing.assert_allclose(a.rollouts("noise"), b.rollouts("noise"), rtol=1e-12, atol=1e-13)

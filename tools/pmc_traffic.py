@@ -38,8 +38,10 @@ def main():
         e = {c: round(v, 3) for c, v in d.items()}
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             e["fetch_bytes_corrected"] = 2.0 * d["FETCH_SIZE"] * 1024
+            e["fetch_bytes_uncorrected"] = d["FETCH_SIZE"] * 1024
             e["write_bytes"] = d["WRITE_SIZE"] * 1024
             e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+            e["hbm_bytes_uncorrected"] = e["fetch_bytes_uncorrected"] + e["write_bytes"]
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             e["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0), 4)
         kernels[k] = e
@@ -47,10 +49,14 @@ def main():
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE TCC_HIT_sum TCC_MISS_sum | SQ_* (separate passes), "
                   "bench.py --steps 40 --warmup 5 --no-timing; per-dispatch means",
-        "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> B; Infinity-Cache hits are "
-                      "counted (memory side of L2), so this is L2-miss traffic, an upper bound on HBM bytes",
+        "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B, MI355X_MICROARCH.md:298, calibrated "
+                      "for wide coalesced reads); the SDF gathers are 4-B lane loads, for which the factor is "
+                      "uncalibrated, so the uncorrected figure (x1) is reported beside it: the true bytes lie "
+                      "between the two.  KiB -> B; Infinity-Cache hits are counted (memory side of L2), so this is "
+                      "L2-miss traffic, an upper bound on HBM bytes",
         "stage": "rollout_cost = k_rollout",
         "hbm_bytes_per_launch": sum(kernels[k].get("hbm_bytes", 0.0) for k in stage),
+        "hbm_bytes_per_launch_uncorrected": sum(kernels[k].get("hbm_bytes_uncorrected", 0.0) for k in stage),
         "kernels": kernels,
     }
     with open(out, "w") as f:
