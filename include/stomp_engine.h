@@ -239,6 +239,11 @@ int stomp_device_count(int32_t* count);
 
 /* RCCL unique id for world_size > 1 (call on rank 0, broadcast the 128 bytes). */
 int stomp_comm_unique_id(void* out128);
+/* Id of an in-process exchange group of world_size ranks: the ranks are engines of THIS
+ * process (on one device or several), each created with this id, its rank and world_size and
+ * each driven by a host thread of its own; the per-iteration exchanges are device-to-device
+ * copies ordered by HIP events instead of RCCL (same results bit for bit). */
+int stomp_comm_local_id(int32_t world_size, void* out128);
 
 /* deterministic math + RNG primitives evaluated on the device (parity tests) */
 int stomp_device_selftest(const double* x, int32_t n, double* out_exp, double* out_log, double* out_sin,

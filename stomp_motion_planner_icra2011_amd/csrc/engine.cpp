@@ -10,7 +10,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -34,6 +39,50 @@ thread_local std::string g_last_error;
 enum TimerId { T_NOISE = 0, T_COST, T_WEIGHTS, T_UPDATE, T_NOISELESS, T_REUSE, T_TERMS, T_PREGEN, T_COUNT };
 const char* kTimerNames[T_COUNT] = {"noise", "rollout_cost", "weights", "update", "noiseless", "reuse", "state_terms",
                                     "pregen"};
+
+// In-process exchange group: the ranks of one sharded problem as engines of ONE process, each
+// driven by its own host thread (one per device, or several on one device).  The collectives are
+// device-to-device copies on the ranks' own streams, ordered by HIP events and two host barriers
+// per collective (publish -> copy -> done), in place of RCCL.  Created by stomp_comm_local_id.
+constexpr char kLocalMagic[8] = {'S', 'T', 'O', 'M', 'P', 'L', 'O', 'C'};
+
+struct LocalGroup {
+    int world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    struct Slot {
+        const void* src = nullptr;
+        hipEvent_t ready = nullptr, done = nullptr;
+        int device = 0;
+    };
+    std::vector<Slot> slot;
+    std::vector<char> joined;
+    long long phase = 0;    // completed barrier phases
+    int arrived = 0;
+    bool broken = false;    // a rank timed out: every later barrier fails at once
+    // all ranks arrive (or the wait times out: a rank not driven from a thread of its own)
+    bool barrier(std::unique_lock<std::mutex>& lk)
+    {
+        if (broken) return false;
+        const long long my = phase;
+        if (++arrived == world) {
+            arrived = 0;
+            ++phase;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return phase != my || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
+std::mutex g_groups_mu;
+std::map<uint64_t, std::shared_ptr<LocalGroup>> g_groups;   // created, not yet joined by every rank
+uint64_t g_next_group = 1;
 
 }  // namespace
 
@@ -108,20 +157,13 @@ struct stomp_engine {
 #ifdef STOMP_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
+    std::shared_ptr<LocalGroup> local;   // in-process exchange group (stomp_comm_local_id), or null
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    double* d_mm_all = nullptr;          // [world][2][J][N] gathered (max, -min) of a local group
 };
 
 namespace {
 
-// a communicator exists: world > 1, or the one-rank RCCL hook
-bool has_comm(const stomp_engine* e)
-{
-#ifdef STOMP_WITH_RCCL
-    return e->comm != nullptr;
-#else
-    (void)e;
-    return false;
-#endif
-}
 
 int fail(stomp_engine* e, int code, const char* fmt, ...)
 {
@@ -356,6 +398,8 @@ void release(stomp_engine* e)
 #ifdef STOMP_WITH_RCCL
     if (e->comm) ncclCommDestroy(e->comm);
 #endif
+    if (e->ev_ready) hipEventDestroy(e->ev_ready);
+    if (e->ev_done) hipEventDestroy(e->ev_done);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
 }
 
@@ -409,6 +453,7 @@ int flush_noiseless(stomp_engine* e)
     return 0;
 }
 
+
 #ifdef STOMP_WITH_RCCL
 #define NCCL_TRY(e, x)                                                                       \
     do {                                                                                     \
@@ -416,6 +461,66 @@ int flush_noiseless(stomp_engine* e)
         if (_r != ncclSuccess) return fail((e), STOMP_E_COMM, "%s: %s", #x, ncclGetErrorString(_r)); \
     } while (0)
 #endif
+
+// all-gather of n doubles per rank, rank order, over the in-process group: publish the send
+// buffer with an event recorded after its producer; after the first barrier every rank copies
+// every rank's buffer behind that rank's event; after the second barrier every rank's stream
+// waits for every rank's copies, so no rank overwrites a buffer another still reads
+int local_gather(stomp_engine* e, const double* send, double* recv, size_t n)
+{
+    LocalGroup& g = *e->local;
+    HIP_TRY(e, hipEventRecord(e->ev_ready, e->stream));
+    std::unique_lock<std::mutex> lk(g.mu);
+    g.slot[e->rank].src = send;
+    g.slot[e->rank].ready = e->ev_ready;
+    g.slot[e->rank].done = e->ev_done;
+    if (!g.barrier(lk)) return fail(e, STOMP_E_COMM, "local exchange group: a rank did not arrive (each rank needs a host thread of its own)");
+    std::vector<LocalGroup::Slot> sl = g.slot;
+    lk.unlock();
+    for (int q = 0; q < g.world; ++q) {
+        if (q != e->rank) HIP_TRY(e, hipStreamWaitEvent(e->stream, sl[q].ready, 0));
+        HIP_TRY(e, hipMemcpyAsync(recv + (size_t)q * n, sl[q].src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
+    }
+    HIP_TRY(e, hipEventRecord(e->ev_done, e->stream));
+    lk.lock();
+    if (!g.barrier(lk)) return fail(e, STOMP_E_COMM, "local exchange group: a rank did not arrive");
+    lk.unlock();
+    for (int q = 0; q < g.world; ++q)
+        if (q != e->rank) HIP_TRY(e, hipStreamWaitEvent(e->stream, sl[q].done, 0));
+    return 0;
+}
+
+// all-reduce(max) in place of n doubles over the ranks (RCCL, or the in-process group; with one
+// rank the identity)
+int exchange_max(stomp_engine* e, double* buf, size_t n)
+{
+#ifdef STOMP_WITH_RCCL
+    if (e->comm) {
+        NCCL_TRY(e, ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, e->comm, e->stream));
+        return 0;
+    }
+#endif
+    if (e->local) {
+        int rc = local_gather(e, buf, e->d_mm_all, n);
+        if (rc) return rc;
+        launch_gather_max(e->d_mm_all, e->world, (int)n, buf, e->stream);
+    }
+    return 0;
+}
+
+// all-gather of n doubles per rank into recv [world][n]
+int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
+{
+#ifdef STOMP_WITH_RCCL
+    if (e->comm) {
+        NCCL_TRY(e, ncclAllGather(send, recv, n, ncclFloat64, e->comm, e->stream));
+        return 0;
+    }
+#endif
+    if (e->local) return local_gather(e, send, recv, n);
+    HIP_TRY(e, hipMemcpyAsync(recv, send, sizeof(double) * n, hipMemcpyDeviceToDevice, e->stream));
+    return 0;
+}
 
 // generateRollouts' sampling arguments of iteration it (policy_improvement_loop.cpp:155-160:
 // sigma_d * decay_d^(it - 1))
@@ -547,28 +652,14 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             const size_t nb_loc = (size_t)e->K_loc / kSumBlock;
             wa.mode = W_MINMAX;
             launch_weights(wa, e->stream, carry);
-#ifdef STOMP_WITH_RCCL
-            if (e->comm)
-                NCCL_TRY(e, ncclAllReduce(e->d_mm, e->d_mm, 2 * JN, ncclFloat64, ncclMax, e->comm, e->stream));
-#endif
+            int rc = exchange_max(e, e->d_mm, 2 * JN);
+            if (rc) return rc;
             wa.mode = W_PSUM;
             launch_weights(wa, e->stream);
-#ifdef STOMP_WITH_RCCL
-            if (e->comm)
-                NCCL_TRY(e, ncclAllGather(e->d_psum_part, e->d_psum_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
-#endif
-            if (!has_comm(e))
-                HIP_TRY(e, hipMemcpyAsync(e->d_psum_all, e->d_psum_part, sizeof(double) * nb_loc * JN,
-                                          hipMemcpyDeviceToDevice, e->stream));
+            if ((rc = exchange_gather(e, e->d_psum_part, e->d_psum_all, nb_loc * JN))) return rc;
             wa.mode = W_USUM;
             launch_weights(wa, e->stream);
-#ifdef STOMP_WITH_RCCL
-            if (e->comm)
-                NCCL_TRY(e, ncclAllGather(e->d_u_part, e->d_u_all, nb_loc * JN, ncclFloat64, e->comm, e->stream));
-#endif
-            if (!has_comm(e))
-                HIP_TRY(e, hipMemcpyAsync(e->d_u_all, e->d_u_part, sizeof(double) * nb_loc * JN,
-                                          hipMemcpyDeviceToDevice, e->stream));
+            if ((rc = exchange_gather(e, e->d_u_part, e->d_u_all, nb_loc * JN))) return rc;
         }
     }
     {
@@ -654,7 +745,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         if (d->num_rollouts % (world * kSumBlock) != 0)
             return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be a multiple of 64 * world_size");
 #ifndef STOMP_WITH_RCCL
-        return fail(nullptr, STOMP_E_UNSUPPORTED, "built without RCCL");
+        if (std::memcmp(d->comm_id, kLocalMagic, sizeof kLocalMagic) != 0)
+            return fail(nullptr, STOMP_E_UNSUPPORTED, "built without RCCL (use stomp_comm_local_id)");
 #endif
     }
 
@@ -983,13 +1075,49 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     hipMemcpyAsync(e->d_last_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
     hipMemcpyAsync(e->d_best_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
 
+    const bool local_id = world > 1 && std::memcmp(d->comm_id, kLocalMagic, sizeof kLocalMagic) == 0;
+    if (local_id) {
+        uint64_t gid = 0;
+        std::memcpy(&gid, (const char*)d->comm_id + 8, sizeof gid);
+        std::shared_ptr<LocalGroup> g;
+        {
+            std::lock_guard<std::mutex> lk(g_groups_mu);
+            auto it = g_groups.find(gid);
+            if (it != g_groups.end()) g = it->second;
+        }
+        if (!g) CREATE_TRY(fail(e, STOMP_E_COMM, "unknown local exchange group (stomp_comm_local_id)"));
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            if (g->world != world) CREATE_TRY(fail(e, STOMP_E_COMM, "local group of %d ranks, engine world_size %d",
+                                                   g->world, world));
+            if (g->joined[e->rank]) CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d joined the local group twice", e->rank));
+            g->joined[e->rank] = 1;
+            g->slot[e->rank].device = e->device;
+            for (int q = 0; q < world; ++q)   // copies between the ranks' devices go peer to peer
+                if (g->joined[q] && g->slot[q].device != e->device) {
+                    (void)hipDeviceEnablePeerAccess(g->slot[q].device, 0);
+                    (void)hipGetLastError();   // already enabled is fine
+                }
+            bool all = true;
+            for (int q = 0; q < world; ++q) all = all && g->joined[q];
+            if (all) {
+                std::lock_guard<std::mutex> lk2(g_groups_mu);
+                g_groups.erase(gid);   // every rank holds it now
+            }
+        }
+        e->local = g;
+        if (hipEventCreateWithFlags(&e->ev_ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_done, hipEventDisableTiming) != hipSuccess)
+            CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipEventCreate failed"));
+        CREATE_TRY(dev_alloc(e, &e->d_mm_all, (size_t)world * 2 * J * N));
+    }
 #ifdef STOMP_WITH_RCCL
-    if (world > 1) {
+    if (world > 1 && !local_id) {
         ncclUniqueId id;
         std::memcpy(&id, d->comm_id, sizeof id);
         if (ncclCommInitRank(&e->comm, world, id, e->rank) != ncclSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "ncclCommInitRank failed"));
-    } else if (e->split_modes) {
+    } else if (e->split_modes && world == 1) {
         // STOMP_DEBUG_RCCL_ONE_RANK=1 (with the sharded-modes hook): a one-rank communicator,
         // so the sharded path's RCCL all-reduce / all-gathers run on a one-GPU box
         const char* one = std::getenv("STOMP_DEBUG_RCCL_ONE_RANK");
@@ -1417,6 +1545,26 @@ int stomp_device_count(int32_t* count)
     int n = 0;
     hipError_t st = hipGetDeviceCount(&n);
     *count = st == hipSuccess ? n : 0;
+    return 0;
+}
+
+int stomp_comm_local_id(int32_t world_size, void* out128)
+{
+    if (world_size < 1 || !out128) return fail(nullptr, STOMP_E_INVALID, "invalid local group arguments");
+    auto g = std::make_shared<LocalGroup>();
+    g->world = world_size;
+    g->slot.resize(world_size);
+    g->joined.assign(world_size, 0);
+    uint64_t gid;
+    {
+        std::lock_guard<std::mutex> lk(g_groups_mu);
+        gid = g_next_group++;
+        g_groups[gid] = g;
+    }
+    std::memset(out128, 0, 128);
+    std::memcpy(out128, kLocalMagic, sizeof kLocalMagic);
+    std::memcpy((char*)out128 + 8, &gid, sizeof gid);
+    std::memcpy((char*)out128 + 16, &world_size, sizeof world_size);
     return 0;
 }
 

@@ -51,6 +51,23 @@ __global__ void k_pad_fk(DevModel m, const double* start, const double* goal, do
     if (col) atomicOr(pad_cf, 1);
 }
 
+__global__ void k_gather_max(const double* g, int world, int n, double* out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double v = g[i];
+    for (int r = 1; r < world; ++r) {
+        const double x = g[(size_t)r * n + i];
+        v = x > v ? x : v;
+    }
+    out[i] = v;
+}
+
+void launch_gather_max(const double* gathered, int world, int n, double* out, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_gather_max, dim3((n + 255) / 256), dim3(256), 0, s, gathered, world, n, out);
+}
+
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s)
 {

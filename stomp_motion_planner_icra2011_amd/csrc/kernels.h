@@ -274,6 +274,8 @@ bool weights_carry_pregen(int K_loc);
 int weights_tile(int K_loc);
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
                    double* theta, const int* stop, hipStream_t s);
+// out[i] = max over r < world of gathered[r][i] (the in-process group's all-reduce(max))
+void launch_gather_max(const double* gathered, int world, int n, double* out, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);
 void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,

@@ -81,7 +81,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_engine_get_matrix", "stomp_engine_get_pad_positions", "stomp_engine_set_timing",
             "stomp_engine_get_timing", "stomp_engine_local_rollouts", "stomp_sdf_build", "stomp_comm_unique_id",
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
-            "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules"]
+            "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id"]
 
 _lib = None
 
@@ -122,6 +122,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_sdf_build.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double, dp, C.c_int32, dp,
                                   C.c_int32, C.c_void_p, C.c_void_p]
     l.stomp_comm_unique_id.argtypes = [C.c_void_p]
+    l.stomp_comm_local_id.argtypes = [C.c_int32, C.c_void_p]
     l.stomp_device_alloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
     l.stomp_device_free.argtypes = [C.c_void_p]
     l.stomp_device_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
@@ -374,6 +375,13 @@ def device_count() -> int:
 def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(load_library().stomp_comm_unique_id(buf))
+    return buf.raw
+
+
+def comm_local_id(world_size: int) -> bytes:
+    """Id of an in-process exchange group (ranks = engines of this process, one host thread each)."""
+    buf = C.create_string_buffer(128)
+    _check(load_library().stomp_comm_local_id(world_size, buf))
     return buf.raw
 
 

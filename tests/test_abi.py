@@ -102,3 +102,17 @@ def test_abi_version_mismatch_rejected():
     assert lib.stomp_engine_create(C.byref(d), C.byref(h)) == -1
     assert b"abi_version" in lib.stomp_last_error()
     assert not h.value
+
+
+@pytest.mark.parametrize("rank,comm,msg", [(0, None, "needs a comm_id"), (2, b"\0" * 128, "outside [0, world_size 2)"),
+                                           (-1, b"\0" * 128, "outside")])
+def test_multi_rank_arguments_checked(rank, comm, msg):
+    p = pb.make_problem(grid_n=16, num_rollouts=128, num_reused_rollouts=0)
+    with pytest.raises(RuntimeError) as ei:
+        eng.Engine(p, rank=rank, world_size=2, comm_id=comm)
+    assert msg in str(ei.value)
+
+
+def test_local_group_ids_are_distinct():
+    a, b = eng.comm_local_id(2), eng.comm_local_id(2)
+    assert a[:8] == b"STOMPLOC" and b[:8] == b"STOMPLOC" and a != b and len(a) == 128
