@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define STOMP_ENGINE_ABI_VERSION 2
+#define STOMP_ENGINE_ABI_VERSION 3
 
 #define STOMP_OK 0
 #define STOMP_E_INVALID (-1)   /* bad sizes / arguments */
@@ -162,7 +162,11 @@ typedef struct stomp_iter_out {
     int32_t constraints_satisfied; /* last_trajectory_constraints_satisfied_ */
 } stomp_iter_out;
 
-/* STOMPStatistics (msg/STOMPStatistics.msg) without the ROS header / torques */
+/* STOMPStatistics (msg/STOMPStatistics.msg): the per-iteration costs go to the
+ * costs_per_iteration argument of stomp_engine_optimize, the torques to
+ * stomp_engine_get_best_torques.  Durations are seconds from the loop's start to the end of
+ * the noiseless rollout of (collision_)success_iteration, on the device wall clock
+ * (stomp_optimizer.cpp:251, 306-319); 0 when that iteration never came. */
 typedef struct stomp_stats {
     int32_t iterations;
     int32_t success;
@@ -170,6 +174,8 @@ typedef struct stomp_stats {
     int32_t collision_success_iteration;
     int32_t last_improvement_iteration;
     double best_cost;
+    double success_duration;
+    double collision_success_duration;
 } stomp_stats;
 
 int stomp_engine_create(const stomp_engine_desc* desc, stomp_engine** out);
@@ -196,6 +202,31 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
                       uint8_t* constraints_satisfied);
 
 int stomp_engine_optimize(stomp_engine* e, stomp_stats* stats, double* costs_per_iteration);
+/* STOMPStatistics.torques after optimize (stomp_optimizer.cpp:384-398): per free waypoint,
+ * sum_j |tau_j| of the best trajectory by inverse dynamics over the torque chain (N doubles).
+ * Needs the segment inertias in the descriptor (also with the torque term off);
+ * STOMP_E_UNSUPPORTED without them. */
+int stomp_engine_get_best_torques(stomp_engine* e, double* torques);
+
+/* PolicyImprovement (policy_improvement.h:86-126) step by step, for a caller that executes the
+ * rollouts with its own Task between the steps (single rank):
+ *   get_rollouts        generateRollouts(noise_stddev) + computeProjectedNoise (:158-260): reuse
+ *                       ranking, new noise for the generated rows keyed by `iteration` (the
+ *                       Philox stream of runSingleIteration(iteration)); the K_gen generated
+ *                       parameter sets (K_gen x J x N) and K_gen out
+ *   set_rollout_costs   setRolloutCosts (:262-281): state costs of the generated rows (K x N,
+ *                       rows >= K_gen ignored), control costs of all K with 0.5 * weight,
+ *                       Rollout::getCost of every row (K) out
+ *   improve_policy      improvePolicy (:385-401): probabilities and the update M (sum eps P)
+ *                       (J x N; row 0 of the reference's per-joint update matrices), theta untouched
+ *   add_extra_rollouts  addExtraRollouts (:443-462) of num = 1 rollout: parameters J x N and its
+ *                       state costs N; noise against the current theta
+ * Applying the update is Policy::updateParameters: stomp_engine_get_theta / set_theta. */
+int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* noise_stddev, double* rollouts,
+                          int32_t* num_generated);
+int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double control_cost_weight, double* totals);
+int stomp_pi_improve_policy(stomp_engine* e, double* updates);
+int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* params, const double* costs);
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj);
 int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
 
@@ -206,7 +237,8 @@ int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
 int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out);
 /* which: "Rinv","L","M","Qinv" (N x N, joint selects Qinv), "R" (free block of the
  * control-cost matrix, CovariantTrajectoryPolicy::getControlCosts,
- * covariant_trajectory_policy.h:235-239) */
+ * covariant_trajectory_policy.h:235-239), "D0","D1","D2" (the policy's differentiation
+ * matrices, (N+12) x (N+12), covariant_trajectory_policy.cpp:204-226).  Host only. */
 int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, double* out);
 /* sphere world positions at the 12 padding points (12 x S x 3) */
 int stomp_engine_get_pad_positions(stomp_engine* e, double* out);

@@ -6,6 +6,7 @@
 //   Task                       include/stomp_motion_planner/task.h:49-93
 //   Policy                     include/stomp_motion_planner/policy.h:47-134
 //   CovariantTrajectoryPolicy  include/stomp_motion_planner/covariant_trajectory_policy.h:56-146
+//   PolicyImprovement          include/stomp_motion_planner/policy_improvement.h:65-126
 //   PolicyImprovementLoop      include/stomp_motion_planner/policy_improvement_loop.h:52-98
 //   StompOptimizer             include/stomp_motion_planner/stomp_optimizer.h:63-213
 // What changes at the boundary (no ROS, Eigen 2, KDL or boost in this build):
@@ -13,8 +14,11 @@
 //   * boost::shared_ptr -> std::shared_ptr; ros::NodeHandle arguments are dropped (the
 //     values the reference reads from the parameter server arrive in StompParameters)
 //   * the KDL tree / collision points / distance field arrive as plain tables
-//     (StompRobotModel, StompCollisionSpace), the ROS publishers and path constraints
-//     are not taken (the engine has no visualisation and no constraint term yet)
+//     (StompRobotModel, StompCollisionSpace); orientation path constraints arrive as
+//     Constraints; the ROS publishers are not taken (no visualisation)
+//   * the rollouts, the policy parameters and the PolicyImprovement state live in HBM inside
+//     one engine; PolicyImprovement therefore works on the policy of a StompOptimizer, and
+//     the rollout counts / time steps are fixed when that optimizer (its engine) is created
 // Failures return false and leave the reason in lastError() (the reference logs with
 // ROS_ERROR and returns false).  One optimizer owns one engine (one HIP device stream).
 #ifndef STOMP_MOTION_PLANNER_STOMP_FACADE_H
@@ -110,6 +114,14 @@ public:
     virtual bool updateParameters(const std::vector<MatrixXd>& updates) = 0;
     virtual bool getParameters(std::vector<VectorXd>& parameters) = 0;
     virtual bool setParameters(const std::vector<VectorXd>& parameters) = 0;
+    // policy.h:128-131: control costs of time-varying parameters [J][T] N (summed over T), and of
+    // one parameter set plus noise ([J] N each); weight multiplies every squared derivative
+    virtual bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices,
+                                     const std::vector<std::vector<VectorXd>>& parameters, const double weight,
+                                     std::vector<VectorXd>& control_costs) = 0;
+    virtual bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices,
+                                     const std::vector<VectorXd>& parameters, const std::vector<VectorXd>& noise,
+                                     const double weight, std::vector<VectorXd>& control_costs) = 0;
 };
 
 class StompOptimizer;
@@ -127,9 +139,23 @@ public:
     bool updateParameters(const std::vector<MatrixXd>& updates) override;
     bool getParameters(std::vector<VectorXd>& parameters) override;
     bool setParameters(const std::vector<VectorXd>& parameters) override;
+    // covariant_trajectory_policy.cpp:228-304 on the host (the engine prices its own rollouts
+    // inside the iteration): x = the padded trajectory (start / goal rows) with the free part
+    // set, costs_all += (weight * derivative_cost_i) * (D_i x)^2, the padding costs folded
+    // into the first / last free entries
+    bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices,
+                             const std::vector<std::vector<VectorXd>>& parameters, const double weight,
+                             std::vector<VectorXd>& control_costs) override;
+    bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices, const std::vector<VectorXd>& parameters,
+                             const std::vector<VectorXd>& noise, const double weight,
+                             std::vector<VectorXd>& control_costs) override;
+    StompOptimizer* owner() const { return owner_; }
 
 private:
+    bool loadDifferentiation();
+    void accumulateCosts(int d, const VectorXd& free, const double weight, VectorXd& costs_all) const;
     StompOptimizer* owner_;
+    std::vector<MatrixXd> D_;      // differentiation matrices (N+12)^2, covariant_trajectory_policy.cpp:204-226
 };
 
 class Task {
@@ -140,16 +166,23 @@ public:
     virtual bool getPolicy(std::shared_ptr<Policy>& policy) = 0;
     virtual bool setPolicy(const std::shared_ptr<Policy> policy) = 0;
     virtual bool getControlCostWeight(double& control_cost_weight) = 0;
+    // Not in the reference's Task: execute() of a batch of rollouts ([E][J] N -> [E] N), which
+    // PolicyImprovementLoop calls; the default executes them one by one
+    virtual bool executeBatch(std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
+                              const int iteration_number);
 };
 
-struct STOMPStatistics {   // msg/STOMPStatistics.msg without the ROS header / torques
+struct STOMPStatistics {   // msg/STOMPStatistics.msg without the ROS header
     int iterations = 0;
     bool success = false;
     int success_iteration = -1;
+    double success_duration = 0.0;             // seconds from the loop's start (device wall clock)
     int collision_success_iteration = -1;
+    double collision_success_duration = 0.0;
     int last_improvement_iteration = -1;
     double best_cost = 0.0;
-    std::vector<double> costs;   // last_trajectory_cost_ per iteration
+    std::vector<double> costs;     // last_trajectory_cost_ per iteration
+    std::vector<double> torques;   // per free waypoint, sum |tau| of the best trajectory (empty without inertias)
 };
 
 class StompOptimizer : public Task {
@@ -174,7 +207,10 @@ public:
     bool setPolicy(const std::shared_ptr<Policy> policy) override;
     bool getControlCostWeight(double& control_cost_weight) override;
 
-    // batched Task::execute: parameters [E][J] N -> costs [E] N, collision flags
+    // batched Task::execute: parameters [E][J] N -> costs [E] N (one engine launch)
+    bool executeBatch(std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
+                      const int iteration_number) override;
+    // ... and the collision flags
     bool executeBatch(const std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
                       std::vector<bool>& collision_free, const int iteration_number);
 
@@ -189,8 +225,12 @@ public:
     bool lastTrajectoryCollisionFree() const { return last_cf_; }
     bool lastTrajectoryConstraintsSatisfied() const { return last_cs_; }
 
+    const StompParameters& parameters() const { return *parameters_; }
+    const StompTrajectory& trajectory() const { return *trajectory_; }
+
 private:
     friend class PolicyImprovementLoop;
+    friend class PolicyImprovement;
     friend class CovariantTrajectoryPolicy;
     bool check(int rc);
     StompTrajectory* trajectory_;
@@ -205,17 +245,67 @@ private:
     std::string error_;
 };
 
-// policy_improvement_loop.cpp:88-202.  The loop drives the engine's fused iteration, so
-// the task must be a StompOptimizer (the reference loop only ever runs that task).
+// policy_improvement.h:65-126 / policy_improvement.cpp:64-489 over the engine's rollout set
+// (stomp_pi_* of the C ABI).  The policy must be the CovariantTrajectoryPolicy of a
+// StompOptimizer: its rollouts, noise generators and projection matrices live in that engine.
+class PolicyImprovement {
+public:
+    bool initialize(const int num_rollouts, const int num_time_steps, const int num_reused_rollouts,
+                    const int num_extra_rollouts, std::shared_ptr<Policy> policy, bool use_cumulative_costs = true);
+    // the counts are fixed when the engine is created: accepted when they match it
+    bool setNumRollouts(const int num_rollouts, const int num_reused_rollouts, const int num_extra_rollouts);
+    // the K_gen new rollouts [K_gen][J] N; noise_stddev per joint
+    bool getRollouts(std::vector<std::vector<VectorXd>>& rollouts, const std::vector<double>& noise_stddev);
+    // costs: num_rollouts x N state costs (rows >= K_gen ignored); totals: Rollout::getCost of all K
+    bool setRolloutCosts(const MatrixXd& costs, const double control_cost_weight,
+                         std::vector<double>& rollout_costs_total);
+    // [J] N x N matrices, row 0 = the update (policy_improvement.cpp:370-383)
+    bool improvePolicy(std::vector<MatrixXd>& parameter_updates);
+    bool addExtraRollouts(std::vector<std::vector<VectorXd>>& rollouts, std::vector<VectorXd>& rollout_costs);
+    // The noise of getRollouts is a counter-based stream keyed by an iteration number (the
+    // reference's generators are stateful); each getRollouts uses the current key and advances
+    // it by one, starting at 1.  PolicyImprovementLoop sets it to runSingleIteration's number.
+    void setNoiseIteration(int iteration) { noise_iteration_ = iteration; }
+    const std::string& lastError() const { return error_; }
+
+private:
+    bool check(int rc);
+    std::shared_ptr<Policy> policy_;
+    StompOptimizer* owner_ = nullptr;
+    stomp_engine* engine_ = nullptr;
+    int J_ = 0, N_ = 0, K_ = 0, K_gen_ = 0, noise_iteration_ = 1;
+    bool initialized_ = false;
+    std::string error_;
+};
+
+// policy_improvement_loop.cpp:88-202.  Drives any Task: getRollouts, Task::executeBatch,
+// setRolloutCosts, improvePolicy, updateParameters, the noiseless execute and addExtraRollouts,
+// as the reference does.  When the task is a StompOptimizer the whole iteration runs as the
+// engine's fused launch sequence instead (stomp_engine_iterate, bit-identical results), unless
+// setUseFusedIteration(false).  The loop parameters (rollout counts, noise schedule) are the
+// ones of the StompOptimizer that owns the task's policy (the reference reads the same
+// params.yaml values from the node handle, policy_improvement_loop.cpp:112-123).
 class PolicyImprovementLoop {
 public:
     bool initialize(std::shared_ptr<Task> task);
     bool runSingleIteration(int iteration_number);
+    void setUseFusedIteration(bool on) { fused_ = on; }
     const std::string& lastError() const { return error_; }
 
 private:
+    bool runGeneric(int iteration_number);
     std::shared_ptr<Task> task_;
-    StompOptimizer* optimizer_ = nullptr;
+    std::shared_ptr<Policy> policy_;
+    StompOptimizer* optimizer_ = nullptr;   // the task, when it is a StompOptimizer
+    StompOptimizer* owner_ = nullptr;       // the optimizer owning the policy
+    PolicyImprovement policy_improvement_;
+    bool fused_ = true;
+    int num_rollouts_ = 0, num_time_steps_ = 0;
+    std::vector<double> noise_stddev_, noise_decay_;
+    double control_cost_weight_ = 0.0;
+    std::vector<std::vector<VectorXd>> rollouts_;
+    std::vector<MatrixXd> parameter_updates_;
+    std::vector<VectorXd> parameters_;
     std::string error_;
 };
 

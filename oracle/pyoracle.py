@@ -94,6 +94,7 @@ def lib():
         l.so_iterate.argtypes = [P, C.c_int, C.POINTER(so_iter_out)]
         l.so_optimize.argtypes = [P, C.POINTER(so_stats), dp]
         l.so_get_best_trajectory.argtypes = [P, dp]
+        l.so_get_best_torques.argtypes = [P, dp]
         l.so_get_last_trajectory.argtypes = [P, dp]
         l.so_get_rollouts.argtypes = [P, C.c_char_p, dp]
         l.so_philox4x32.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
@@ -252,6 +253,12 @@ class Oracle:
     def best_trajectory(self) -> np.ndarray:
         out = np.zeros((self.J, self.N))
         lib().so_get_best_trajectory(self.h, _dp(out))
+        return out
+
+    def best_torques(self) -> np.ndarray:
+        out = np.zeros(self.N)
+        if lib().so_get_best_torques(self.h, _dp(out)) != 0:
+            raise RuntimeError(lib().so_last_error().decode())
         return out
 
     def last_trajectory(self) -> np.ndarray:

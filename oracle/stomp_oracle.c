@@ -380,7 +380,7 @@ static void rb_inertia(const so_inertia* in, double* m, double* h, double* I)
 
 int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, const double* qdd, double* tau)
 {
-    if (!P->torque) return -1;
+    if (!P->chain) return -1;
     wrench_t f[64];
     double Rs[64][9];
     const double* g = P->cfg.gravity;
@@ -754,7 +754,9 @@ so_problem* so_create(const so_config* cfg)
     /* the inverse-dynamics chain (stomp_robot_model.cpp:185-189): segments below torque_root
      * up to torque_tip; its joints must be the group's, in order */
     P->torque = cfg->torque_cost_weight > 1e-9;
-    if (P->torque) {
+    /* built whenever the inertias describe a valid chain: the term runs only with the weight
+     * on, the final torque statistics of optimize() always (stomp_optimizer.cpp:384-398) */
+    {
         const char* why = NULL;
         int path[SO_MAX_CHAIN], n = 0;
         if (!cfg->inertias) why = "torque term needs segment inertias";
@@ -772,19 +774,21 @@ so_problem* so_create(const so_config* cfg)
                 if (P->segs[path[i]].q_index >= 0 && P->segs[path[i]].q_index != nj++) why = "torque chain joints must be the group joints in order";
             if (!why && nj != J) why = "torque chain joints must be the group joints in order";
         }
-        if (why) {
+        if (why && P->torque) {
             set_err(why);
             so_destroy(P);
             return NULL;
         }
-        P->nchain = n;
-        P->chain = (int*)malloc(sizeof(int) * (size_t)n);
-        P->rb_m = dalloc((size_t)n);
-        P->rb_h = dalloc((size_t)n * 3);
-        P->rb_I = dalloc((size_t)n * 9);
-        for (int i = 0; i < n; ++i) {
-            P->chain[i] = path[n - 1 - i];
-            rb_inertia(&cfg->inertias[P->chain[i]], &P->rb_m[i], P->rb_h + 3 * i, P->rb_I + 9 * i);
+        if (!why) {
+            P->nchain = n;
+            P->chain = (int*)malloc(sizeof(int) * (size_t)n);
+            P->rb_m = dalloc((size_t)n);
+            P->rb_h = dalloc((size_t)n * 3);
+            P->rb_I = dalloc((size_t)n * 9);
+            for (int i = 0; i < n; ++i) {
+                P->chain[i] = path[n - 1 - i];
+                rb_inertia(&cfg->inertias[P->chain[i]], &P->rb_m[i], P->rb_h + 3 * i, P->rb_I + 9 * i);
+            }
         }
     }
 
@@ -1515,6 +1519,22 @@ int so_optimize(so_problem* P, so_stats* st, double* costs_per_it)
     s.iterations = it;
     s.best_cost = best_cost;
     if (st) *st = s;
+    return 0;
+}
+
+/* STOMPStatistics.torques (stomp_optimizer.cpp:384-398): group_trajectory_ = best, then per free
+ * waypoint sum_j |tau_j| of getTorques */
+int so_get_best_torques(const so_problem* P, double* out)
+{
+    if (!P->chain) { set_err("no torque chain (segment inertias not given)"); return -1; }
+    const int J = P->J, N = P->N, Nall = P->Nall;
+    double* traj = dalloc((size_t)Nall * J);
+    for (int i = 0; i < Nall; ++i)
+        for (int d = 0; d < J; ++d)
+            traj[(size_t)i * J + d] = i < SO_PAD ? P->cfg.start[d]
+                                    : (i >= SO_PAD + N ? P->cfg.goal[d] : P->best_traj[(size_t)d * N + (i - SO_PAD)]);
+    for (int t = 0; t < N; ++t) out[t] = torque_cost_at(P, traj, t + SO_PAD);
+    free(traj);
     return 0;
 }
 

@@ -173,6 +173,8 @@ int so_iterate(so_problem* p, int iteration_number, so_iter_out* out);
 /* StompOptimizer::optimize loop (without the final torque statistics) */
 int so_optimize(so_problem* p, so_stats* stats, double* costs_per_iteration /* may be NULL */);
 int so_get_best_trajectory(const so_problem* p, double* traj /* J x N */);
+/* STOMPStatistics.torques of the best trajectory (N); needs the segment inertias */
+int so_get_best_torques(const so_problem* p, double* torques /* N */);
 int so_get_last_trajectory(const so_problem* p, double* traj /* J x N */);
 
 /* rollout state after so_iterate, for stage tests. which:

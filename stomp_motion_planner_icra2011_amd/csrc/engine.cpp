@@ -157,6 +157,16 @@ struct stomp_engine {
 #ifdef STOMP_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
+    // PolicyImprovement API (stomp_pi_*): the weight the control-cost rows were priced with,
+    // improvePolicy's update (J x N)
+    double pi_weight = 0.0;
+    double* d_delta = nullptr;
+    // STOMPStatistics.torques (stomp_optimizer.cpp:384-398): the torque chain's model whenever
+    // inertias are given (also with the torque term off), its per-waypoint output
+    bool torque_stats = false;
+    TermsModel tq_model{};
+    double *d_tq = nullptr, *d_tq_state = nullptr;
+    int wall_khz = 0;
     std::shared_ptr<LocalGroup> local;   // in-process exchange group (stomp_comm_local_id), or null
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     double* d_mm_all = nullptr;          // [world][2][J][N] gathered (max, -min) of a local group
@@ -549,16 +559,11 @@ NoiseArgs pregen_args(const stomp_engine* e, int it)
     return na;
 }
 
-// One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
-// pipelined: the noiseless rollout of the updated theta is not launched here but evaluated by
-// the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
-int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
+// generateRollouts bookkeeping (policy_improvement.cpp:167-225): the first call generates all K;
+// later ones rank the K previous rollouts and the extra (noiseless) one, keep the best K_r in rows
+// K_gen.. with their noise re-based on the current theta, and generate the rest
+void begin_generate(stomp_engine* e)
 {
-    const int member = it - 1;
-    NoiseArgs na = noise_args(e, it);
-    if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
-
-    // generateRollouts bookkeeping (policy_improvement.cpp:167-175)
     e->K_gen = e->K - e->Kr;
     if (!e->reused_next) {
         e->K_gen = e->K;
@@ -571,6 +576,18 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
                      e->d_tmp_state, e->d_stop, e->stream);
         e->extra_added = false;
     }
+}
+
+// One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
+// pipelined: the noiseless rollout of the updated theta is not launched here but evaluated by
+// the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
+int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
+{
+    const int member = it - 1;
+    NoiseArgs na = noise_args(e, it);
+    if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
+
+    begin_generate(e);
     na.K_gen_global = e->K_gen;
     // generated rows [0, g1 - g0) of this shard: their noise is made by the rollout kernel
     // itself (fused), k_noise only projects and prices the reused rows after them
@@ -924,10 +941,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
 
     // the torque term's chain (stomp_robot_model.cpp:185-189): segments below torque_root up to
-    // torque_tip, whose joints must be the group's joints in order
-    if (d->torque_cost_weight > 1e-9) {
-        std::vector<int> path;
-        torque_chain(d, path);
+    // torque_tip, whose joints must be the group's joints in order.  Built whenever the inertias
+    // describe a valid chain: the term itself runs only with torque_cost_weight > 1e-9, the
+    // final torque statistics of optimize() always (stomp_optimizer.cpp:384-398)
+    std::vector<int> tq_path;
+    const bool tq_chain = torque_chain(d, tq_path) == nullptr;
+    if (tq_chain) {
+        std::vector<int>& path = tq_path;
         std::vector<ChainSeg> cs(path.size());
         for (size_t i = 0; i < path.size(); ++i) {
             cs[i].seg = segs[path[i]];
@@ -946,11 +966,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         ChainSeg* d_chain;
         CREATE_TRY(upload(e, &d_chain, cs.data(), cs.size()));
         TermsModel& t = e->terms;
-        t.torque = 1;
+        t.torque = d->torque_cost_weight > 1e-9 ? 1 : 0;
         t.nchain = (int)cs.size();
         t.chain = d_chain;
         for (int k = 0; k < 3; ++k) t.g[k] = d->gravity[k];
-        e->terms_on = true;
+        if (t.torque) e->terms_on = true;
+        e->torque_stats = true;
     }
     if (d->num_orientation_constraints > 0) {
         std::vector<OcDev> oc(d->num_orientation_constraints);
@@ -978,7 +999,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         e->terms.oc = d_oc;
         e->terms_on = true;
     }
-    if (e->terms_on) {
+    if (e->terms_on || e->torque_stats) {
         TermsModel& t = e->terms;
         t.J = J; t.N = N;
         const double invTime = 1.0 / e->disc, invTime2 = 1.0 / (e->disc * e->disc);   // stomp_trajectory.h:289, 301
@@ -988,10 +1009,23 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         }
         t.start = e->d_start; t.goal = e->d_goal;
         t.w_con = e->w_con; t.w_tq = e->w_tq;
-        if (terms_lds_bytes(t) > 160 * 1024)
-            CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "state-terms kernel needs %zu B of LDS", terms_lds_bytes(t)));
-        CREATE_TRY(dev_alloc(e, &e->d_terms_traj, KJN));
+        if (terms_lds_bytes(t) > 160 * 1024) {
+            if (e->terms_on)
+                CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "state-terms kernel needs %zu B of LDS", terms_lds_bytes(t)));
+            e->torque_stats = false;
+        }
+        if (e->terms_on) CREATE_TRY(dev_alloc(e, &e->d_terms_traj, KJN));
+        if (e->torque_stats) {
+            e->tq_model = t;
+            e->tq_model.torque = 1;
+            e->tq_model.noc = 0;   // torques only
+            CREATE_TRY(dev_alloc(e, &e->d_tq, (size_t)N));
+            CREATE_TRY(dev_alloc(e, &e->d_tq_state, (size_t)N));
+        }
     }
+    CREATE_TRY(dev_alloc(e, &e->d_delta, (size_t)J * N));
+    e->pi_weight = e->w_smooth;
+    if (hipDeviceGetAttribute(&e->wall_khz, hipDeviceAttributeWallClockRate, d->device) != hipSuccess) e->wall_khz = 0;
 
     DevModel& m = e->model;
     m.J = J; m.N = N; m.Nall = e->Nall; m.S = e->S; m.nops = (int)e->ops.size(); m.nseg = e->nseg;
@@ -1052,6 +1086,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
     e->terms.segs = m.segs;
+    e->tq_model.segs = m.segs;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
     m.inv_res = 1.0 / d->grid.resolution;
@@ -1260,6 +1295,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     init.best = 0.0;
     e->h_track[3] = init;
     HIP_TRY(e, hipMemcpyAsync(e->d_track, &e->h_track[3], sizeof(DevTrack), hipMemcpyHostToDevice, e->stream));
+    launch_track_start(e->d_track, e->stream);   // stomp_optimizer.cpp:251 start_time
     const int max_it = e->max_it;
     // host-side generateRollouts state after each iteration, to restore the one the device stopped at
     struct HostState { bool reused_next, extra_added; };
@@ -1323,7 +1359,157 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     s.collision_success_iteration = t.collision_success_iteration;
     s.last_improvement_iteration = t.last_improvement_iteration;
     s.best_cost = t.best;
+    const double tick_s = e->wall_khz > 0 ? 1.0 / (1000.0 * e->wall_khz) : 0.0;
+    s.success_duration = t.success_iteration >= 0 ? (double)(t.t_success - t.t0) * tick_s : 0.0;
+    s.collision_success_duration =
+        t.collision_success_iteration >= 0 ? (double)(t.t_collision_success - t.t0) * tick_s : 0.0;
     if (st) *st = s;
+    return 0;
+}
+
+int stomp_engine_get_best_torques(stomp_engine* e, double* torques)
+{
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
+    if (!e->torque_stats) return fail(e, STOMP_E_UNSUPPORTED, "no torque chain (segment inertias not given)");
+    flush_noiseless(e);
+    HIP_TRY(e, hipMemsetAsync(e->d_tq_state, 0, sizeof(double) * e->N, e->stream));
+    TermsArgs ta{};
+    ta.traj = e->d_best_traj; ta.state = e->d_tq_state; ta.num_noisy = 1; ta.tq_out = e->d_tq;
+    launch_terms(e->tq_model, ta, e->stream);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipMemcpyAsync(torques, e->d_tq, sizeof(double) * e->N, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------- PolicyImprovement API
+// policy_improvement.h:86-126 step by step on the engine's rollout set, for callers that run
+// their own Task::execute between the steps (the fused stomp_engine_iterate does the same work
+// in one launch sequence)
+int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* noise_stddev, double* rollouts,
+                          int32_t* num_generated)
+{
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
+    if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
+    if (!noise_stddev) return fail(e, STOMP_E_INVALID, "null noise_stddev");
+    flush_noiseless(e);
+    begin_generate(e);
+    NoiseArgs na = noise_args(e, iteration);
+    for (int d = 0; d < e->J; ++d) na.sigma.v[d] = noise_stddev[d];   // generateRollouts(noise_stddev)
+    na.stop = nullptr;
+    na.row_begin = 0;
+    na.K_gen_global = e->K_gen;
+    {
+        Timed tm(e, T_NOISE);
+        launch_noise(na, e->stream);
+    }
+    e->pi_weight = e->w_smooth;
+    HIP_TRY(e, hipGetLastError());
+    if (rollouts)
+        HIP_TRY(e, hipMemcpyAsync(rollouts, e->d_params, sizeof(double) * e->K_gen * e->J * e->N,
+                                  hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (num_generated) *num_generated = e->K_gen;
+    return 0;
+}
+
+int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double control_cost_weight, double* totals)
+{
+    if (!e || !costs) return fail(e, STOMP_E_INVALID, "null argument");
+    DeviceGuard dg(e->device);
+    const int K = e->K, J = e->J, N = e->N;
+    // state costs of the generated rows; reused rows keep theirs (policy_improvement.cpp:270-273)
+    HIP_TRY(e, hipMemcpyAsync(e->d_state, costs, sizeof(double) * e->K_gen * N, hipMemcpyHostToDevice, e->stream));
+    if (control_cost_weight != e->pi_weight) {
+        // computeRolloutControlCosts with another weight (:264-266): every row's noise is kept,
+        // its projection and control cost recomputed
+        NoiseArgs na = noise_args(e, 1);
+        na.stop = nullptr; na.row_begin = 0; na.K_gen_global = 0;
+        for (int r = 0; r < 3; ++r) na.wr[r] = 0.5 * control_cost_weight * e->smooth[r];
+        launch_noise(na, e->stream);
+        e->pi_weight = control_cost_weight;
+    }
+    HIP_TRY(e, hipGetLastError());
+    if (totals) {
+        // Rollout::getCost (:149-156): state sum, then each joint's control sum
+        std::vector<double> st((size_t)K * N), ct((size_t)K * J * N);
+        HIP_TRY(e, hipMemcpyAsync(st.data(), e->d_state, sizeof(double) * st.size(), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipMemcpyAsync(ct.data(), e->d_control, sizeof(double) * ct.size(), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        for (int r = 0; r < K; ++r) {
+            const double* sr = st.data() + (size_t)r * N;
+            double c = sr[0];
+            for (int t = 1; t < N; ++t) c += sr[t];
+            for (int d = 0; d < J; ++d) {
+                const double* x = ct.data() + ((size_t)r * J + d) * N;
+                double sd = x[0];
+                for (int t = 1; t < N; ++t) sd += x[t];
+                c += sd;
+            }
+            totals[r] = c;
+        }
+    }
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_pi_improve_policy(stomp_engine* e, double* updates)
+{
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
+    if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
+    WeightArgs wa{};
+    wa.stop = nullptr;
+    wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
+    wa.state = e->d_state; wa.control = e->d_control; wa.noise = e->d_noise;
+    wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
+    wa.tc = weights_tile(e->K_loc);
+    wa.nb_total = e->K / kSumBlock;
+    wa.mode = W_FUSED;
+    {
+        Timed tm(e, T_WEIGHTS);
+        if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
+        launch_weights(wa, e->stream);
+    }
+    {
+        Timed tm(e, T_UPDATE);
+        launch_update(e->J, e->N, e->d_MT, e->d_u, nullptr, e->K / kSumBlock, nullptr, nullptr, e->stream, e->d_delta);
+    }
+    HIP_TRY(e, hipGetLastError());
+    if (updates)
+        HIP_TRY(e, hipMemcpyAsync(updates, e->d_delta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* params, const double* costs)
+{
+    if (!e || !params || !costs) return fail(e, STOMP_E_INVALID, "null argument");
+    DeviceGuard dg(e->device);
+    if (num != 1) return fail(e, STOMP_E_INVALID, "one extra rollout (the loop's noiseless rollout)");
+    const int J = e->J, N = e->N;
+    const size_t JN = (size_t)J * N;
+    // copyParametersFromPolicy, then noise = parameters - theta (policy_improvement.cpp:446-449, 464-469)
+    std::vector<double> th(JN), nz(JN);
+    flush_noiseless(e);
+    HIP_TRY(e, hipMemcpyAsync(th.data(), e->d_theta, sizeof(double) * JN, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    for (size_t k = 0; k < JN; ++k) nz[k] = params[k] - th[k];
+    HIP_TRY(e, hipMemcpyAsync(e->d_x_params, params, sizeof(double) * JN, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->d_x_noise, nz.data(), sizeof(double) * JN, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipMemcpyAsync(e->d_x_state, costs, sizeof(double) * N, hipMemcpyHostToDevice, e->stream));
+    // computeProjectedNoise + computeRolloutControlCosts of the extra row (:452-453)
+    NoiseArgs xa = noise_args(e, 1);
+    xa.stop = nullptr;
+    xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 0; xa.row_begin = 0;
+    for (int r = 0; r < 3; ++r) xa.wr[r] = 0.5 * e->pi_weight * e->smooth[r];
+    xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
+    launch_noise(xa, e->stream);
+    HIP_TRY(e, hipGetLastError());
+    HIP_TRY(e, hipStreamSynchronize(e->stream));   // nz is a pageable host buffer
+    e->extra_added = true;
     return 0;
 }
 
@@ -1387,6 +1573,15 @@ int stomp_engine_get_matrix(stomp_engine* e, const char* which, int32_t joint, d
         for (int i = 0; i < e->N; ++i)
             for (int k = 0; k < e->N; ++k)
                 out[(size_t)i * e->N + k] = e->su.Rall[(size_t)(i + kPad) * e->Nall + k + kPad];
+    } else if (which[0] == 'D' && which[1] >= '0' && which[1] <= '2' && which[2] == 0) {
+        // policy differentiation matrix D_i (Nall x Nall), covariant_trajectory_policy.cpp:204-226
+        const int r = which[1] - '0', A = e->Nall;
+        std::memset(out, 0, sizeof(double) * A * A);
+        for (int i = 0; i < A; ++i)
+            for (int j = 0; j < kDiffRuleLength; ++j) {
+                const int c = i + j - kDiffRuleLength / 2;
+                if (c >= 0 && c < A) out[(size_t)i * A + c] = e->su.dcoef[r][j];
+            }
     } else if (!std::strcmp(which, "Qinv")) {
         if (joint < 0 || joint >= e->J) return fail(e, STOMP_E_INVALID, "joint out of range");
         std::memcpy(out, e->su.Qinv.data() + (size_t)joint * NN, NN * 8);

@@ -171,10 +171,14 @@ __global__ __launch_bounds__(256) void k_track(DevTrack* tr, int it, int max_it_
         const bool cfree = *cf != 0;
         const bool ok = cfree && *cs != 0;
         tr->cfi = ok ? tr->cfi + 1 : 0;
-        if (cfree && tr->collision_success_iteration == -1) tr->collision_success_iteration = it;
+        if (cfree && tr->collision_success_iteration == -1) {
+            tr->collision_success_iteration = it;
+            tr->t_collision_success = wall_clock64();
+        }
         if (ok && tr->success_iteration == -1) {
             tr->success_iteration = it;
             tr->success = 1;
+            tr->t_success = wall_clock64();
         }
         costs[it] = cost;
         copy = 0;
@@ -189,6 +193,16 @@ __global__ __launch_bounds__(256) void k_track(DevTrack* tr, int it, int max_it_
     __syncthreads();
     if (copy)
         for (int i = threadIdx.x; i < JN; i += blockDim.x) best_traj[i] = last_traj[i];
+}
+
+__global__ void k_track_start(DevTrack* tr)
+{
+    if (threadIdx.x == 0) tr->t0 = wall_clock64();
+}
+
+void launch_track_start(DevTrack* tr, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_track_start, dim3(1), dim3(64), 0, s, tr);
 }
 
 void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, const uint8_t* cf, const uint8_t* cs,

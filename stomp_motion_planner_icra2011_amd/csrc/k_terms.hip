@@ -306,6 +306,7 @@ __global__ __launch_bounds__(BLOCK) void k_terms(TermsModel m, TermsArgs a)
             }
         }
         for (int j = 0; j < J; ++j) tq += fabs(Q[J * N + j * N + t]);
+        if (a.tq_out && e == 0) a.tq_out[t] = tq;
     }
     __syncthreads();
     double* cst = F;   // the costs, for the total

@@ -538,7 +538,7 @@ constexpr int kUpdateBatch = UPDATE_BATCH;
 #endif
 
 __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
-                                                int nb_total, double* theta, const int* stop)
+                                                int nb_total, double* theta, const int* stop, double* delta)
 {
     __shared__ double us[256 + 2 * kUpdateBatch];
     const int d = blockIdx.x, i = threadIdx.x;
@@ -567,13 +567,14 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
     band_tile<1, 0, 1, kUpdateBatch, decltype(fill), UPDATE_XPRE>(MT, N, col, 0, N, us, 1, acc, fill);
     const double s = acc[0][0];
     if (i >= N || stopped) return;
-    theta[(size_t)d * N + i] += 1.0 * s;
+    if (delta) delta[(size_t)d * N + i] = s;   // improvePolicy's update alone (PolicyImprovement API)
+    else theta[(size_t)d * N + i] += 1.0 * s;
 }
 
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,
-                   const int* stop, hipStream_t s)
+                   const int* stop, hipStream_t s, double* delta)
 {
-    hipLaunchKernelGGL(k_update, dim3(J), dim3(256), 0, s, J, N, MT, u, u_all, nb_total, theta, stop);
+    hipLaunchKernelGGL(k_update, dim3(J), dim3(256), 0, s, J, N, MT, u, u_all, nb_total, theta, stop, delta);
 }
 
 }  // namespace stomp

@@ -231,6 +231,7 @@ struct TermsArgs {
     double* x_state;
     double* x_total;
     uint8_t* x_cs;
+    double* tq_out;             // [N] sum_j |tau_j| of rollout 0 (STOMPStatistics.torques), or null
 };
 
 // hipFuncAttributeMaxDynamicSharedMemorySize opt-in for more than the default dynamic LDS:
@@ -252,7 +253,13 @@ struct DevTrack {
     int stop, cfi, iterations, success, success_iteration, collision_success_iteration, last_improvement_iteration;
     int pad;
     double best;
+    // device wall clock (wall_clock64, hipDeviceAttributeWallClockRate) at the loop's start and
+    // when the noiseless rollout of success_iteration / collision_success_iteration finished
+    // (STOMPStatistics success_duration / collision_success_duration, stomp_optimizer.cpp:306-319)
+    unsigned long long t0, t_success, t_collision_success;
 };
+// stamps DevTrack::t0 (first launch of an optimize loop)
+void launch_track_start(DevTrack* tr, hipStream_t s);
 void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, const uint8_t* cf, const uint8_t* cs,
                   double* costs, const double* last_traj, double* best_traj, int JN, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
@@ -272,8 +279,9 @@ bool weights_carry_pregen(int K_loc);
 // where the next iteration's pregen rows ride: 1 = the rollout launch (low-priority blocks),
 // 2 = the weights launch (STOMP_PREGEN_HOST=weights)
 int weights_tile(int K_loc);
+// theta += M u; with delta: delta = M u and theta untouched
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
-                   double* theta, const int* stop, hipStream_t s);
+                   double* theta, const int* stop, hipStream_t s, double* delta = nullptr);
 // out[i] = max over r < world of gathered[r][i] (the in-process group's all-reduce(max))
 void launch_gather_max(const double* gathered, int world, int n, double* out, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,

@@ -14,7 +14,7 @@ import numpy as np
 from . import _build
 
 _LIB_PATH = _build.LIB
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class stomp_segment(C.Structure):
@@ -70,7 +70,8 @@ class stomp_iter_out(C.Structure):
 class stomp_stats(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("success", C.c_int32), ("success_iteration", C.c_int32),
                 ("collision_success_iteration", C.c_int32), ("last_improvement_iteration", C.c_int32),
-                ("best_cost", C.c_double)]
+                ("best_cost", C.c_double), ("success_duration", C.c_double),
+                ("collision_success_duration", C.c_double)]
 
 
 # every symbol include/stomp_engine.h declares (checked by tests/test_abi.py)
@@ -81,7 +82,9 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_engine_get_matrix", "stomp_engine_get_pad_positions", "stomp_engine_set_timing",
             "stomp_engine_get_timing", "stomp_engine_local_rollouts", "stomp_sdf_build", "stomp_comm_unique_id",
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
-            "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id"]
+            "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id",
+            "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
+            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts"]
 
 _lib = None
 
@@ -112,6 +115,11 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_eval.argtypes = [P, dp, C.c_int32, dp, C.POINTER(C.c_uint8), dp, C.c_int32, C.POINTER(C.c_uint8)]
     l.stomp_engine_optimize.argtypes = [P, C.POINTER(stomp_stats), dp]
     l.stomp_engine_get_best_trajectory.argtypes = [P, dp]
+    l.stomp_engine_get_best_torques.argtypes = [P, dp]
+    l.stomp_pi_get_rollouts.argtypes = [P, C.c_int32, dp, dp, C.POINTER(C.c_int32)]
+    l.stomp_pi_set_rollout_costs.argtypes = [P, dp, C.c_double, dp]
+    l.stomp_pi_improve_policy.argtypes = [P, dp]
+    l.stomp_pi_add_extra_rollouts.argtypes = [P, C.c_int32, dp, dp]
     l.stomp_engine_get_last_trajectory.argtypes = [P, dp]
     l.stomp_engine_get_rollouts.argtypes = [P, C.c_char_p, dp]
     l.stomp_engine_get_matrix.argtypes = [P, C.c_char_p, C.c_int32, dp]
@@ -307,6 +315,37 @@ class Engine:
         _check(load_library().stomp_engine_get_last_trajectory(self.h, _dp(out)), self.h)
         return out
 
+    def best_torques(self) -> np.ndarray:
+        out = np.zeros(self.N)
+        _check(load_library().stomp_engine_get_best_torques(self.h, _dp(out)), self.h)
+        return out
+
+    # ---------------------------------------------------- PolicyImprovement API (stomp_pi_*)
+    def pi_get_rollouts(self, iteration: int, noise_stddev) -> np.ndarray:
+        sig = np.ascontiguousarray(noise_stddev, np.float64)
+        out = np.zeros((self.K, self.J, self.N))
+        n = C.c_int32()
+        _check(load_library().stomp_pi_get_rollouts(self.h, iteration, _dp(sig), _dp(out), C.byref(n)), self.h)
+        return out[: n.value]
+
+    def pi_set_rollout_costs(self, costs, control_cost_weight: float) -> np.ndarray:
+        c = np.zeros((self.K, self.N))
+        cc = np.asarray(costs, np.float64)
+        c[: cc.shape[0]] = cc
+        totals = np.zeros(self.K)
+        _check(load_library().stomp_pi_set_rollout_costs(self.h, _dp(c), control_cost_weight, _dp(totals)), self.h)
+        return totals
+
+    def pi_improve_policy(self) -> np.ndarray:
+        out = np.zeros((self.J, self.N))
+        _check(load_library().stomp_pi_improve_policy(self.h, _dp(out)), self.h)
+        return out
+
+    def pi_add_extra_rollout(self, params, costs):
+        p = np.ascontiguousarray(params, np.float64)
+        c = np.ascontiguousarray(costs, np.float64)
+        _check(load_library().stomp_pi_add_extra_rollouts(self.h, 1, _dp(p), _dp(c)), self.h)
+
     def rollouts(self, which: str) -> np.ndarray:
         if which.startswith("x_"):
             shape = (self.N,) if which == "x_state_costs" else (self.J, self.N)
@@ -317,7 +356,8 @@ class Engine:
         return out
 
     def matrix(self, which: str, joint: int = 0) -> np.ndarray:
-        out = np.zeros((self.N, self.N))
+        n = self.N + 12 if which in ("D0", "D1", "D2") else self.N
+        out = np.zeros((n, n))
         _check(load_library().stomp_engine_get_matrix(self.h, which.encode(), joint, _dp(out)), self.h)
         return out
 

@@ -29,6 +29,13 @@ def write_problem(p, directory):
                                     float(pr.ridge_factor), int(pr.use_cumulative_costs), int(pr.num_rollouts),
                                     int(pr.num_reused_rollouts), int(p.seed)])))
     rows.append(" ".join(map(repr, [*map(float, p.grid.origin), float(p.grid.resolution)])))
+    # the torque chain (stomp_robot_model.cpp:185-189) and the segment inertias
+    rows.append(" ".join(map(repr, [p.robot.index(p.torque_root), p.robot.index(p.torque_tip),
+                                    *map(float, p.gravity)])))
+    for s in p.robot.segments:
+        inr = s.inertia
+        vals = [inr.mass, *inr.com, *inr.inertia] if inr else [0.0] * 10
+        rows.append(" ".join(map(repr, map(float, vals))))
     prob = os.path.join(directory, "problem.txt")
     with open(prob, "w") as f:
         f.write("\n".join(rows) + "\n")

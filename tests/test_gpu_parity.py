@@ -314,3 +314,63 @@ def test_device_optimize_loop_stops_like_the_reference(K, Kr, after_cf):
         np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f)
     for it in range(est.iterations + 1, est.iterations + 3):
         _compare_iteration(o, e, it)
+
+
+@pytest.mark.parametrize("K,Kr", [(16, 6), (130, 0)])
+def test_policy_improvement_api_bitwise(K, Kr):
+    # the stomp_pi_* entry points driven as policy_improvement_loop.cpp:143-202 drives
+    # PolicyImprovement, with Task::execute through stomp_engine_eval in between
+    p = make(K=K, Kr=Kr)
+    o, e = po.Oracle(p), eng.Engine(p)
+    pr = p.params
+    w = pr.smoothness_cost_weight
+    for it in range(1, 8):
+        sig = np.full(p.J, pr.noise_stddev * pr.noise_decay ** (it - 1))
+        rollouts = e.pi_get_rollouts(it, sig)
+        costs, _, _ = e.execute(rollouts, iteration_member=it - 1)
+        if it == 2:   # another weight re-prices every row; the loop's weight restores it
+            e.pi_set_rollout_costs(costs, 2.0 * w)
+        totals = e.pi_set_rollout_costs(costs, w)
+        upd = e.pi_improve_policy()
+        th = e.theta() + 1.0 * upd   # CovariantTrajectoryPolicy::updateParameters
+        e.set_theta(th)
+        c, cf, _ = e.execute(th, iteration_member=it - 1)
+        e.pi_add_extra_rollout(th, c)
+        oc, ocf = o.iterate(it)
+        assert cf == ocf
+        np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it}")
+        for f in ("params", "noise", "control_costs", "state_costs", "probabilities"):
+            np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f"it {it} {f}")
+        st, ct = o.rollouts("state_costs"), o.rollouts("control_costs")
+        want = []
+        for k in range(K):
+            v = float(st[k][0])
+            for x in st[k][1:]:
+                v += float(x)
+            for row in ct[k]:
+                sd = float(row[0])
+                for x in row[1:]:
+                    sd += float(x)
+                v += sd
+            want.append(v)
+        np.testing.assert_array_equal(totals, want)
+        if Kr:
+            for f in ("x_params", "x_noise", "x_control_costs", "x_state_costs"):
+                np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f"it {it} {f}")
+
+
+def test_optimize_statistics_torques_and_durations():
+    # STOMPStatistics.torques of the best trajectory (stomp_optimizer.cpp:384-398) and the
+    # (collision_)success durations (:306-319)
+    p = make(K=20, Kr=10, grid_n=128, max_iterations=60, max_iterations_after_collision_free=1000)
+    o, e = po.Oracle(p), eng.Engine(p)
+    ost, _ = o.optimize()
+    est, _ = e.optimize()
+    np.testing.assert_array_equal(e.best_torques(), o.best_torques())
+    assert est.success_iteration == ost.success_iteration
+    if est.collision_success_iteration >= 0:
+        assert 0.0 < est.collision_success_duration < 30.0
+    if est.success_iteration >= 0:
+        assert est.collision_success_duration <= est.success_duration < 30.0
+    else:
+        assert est.success_duration == 0.0
