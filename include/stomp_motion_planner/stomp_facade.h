@@ -187,7 +187,7 @@ struct STOMPStatistics {   // msg/STOMPStatistics.msg without the ROS header
 
 class StompOptimizer : public Task {
 public:
-    // stomp_optimizer.cpp:50-70 (publishers and constraints not taken, see the file header)
+    // stomp_optimizer.cpp:50-70 (the ROS publishers are not taken, see the file header)
     StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model, const StompParameters* parameters,
                    StompCollisionSpace* collision_space, const Constraints& constraints = Constraints(),
                    int device = 0, void* stream = nullptr);
