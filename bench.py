@@ -250,7 +250,7 @@ def main():
         return
 
     K = args.rollouts
-    if K % (64 * world) != 0:
+    if world > 1 and K % (64 * world) != 0:
         raise SystemExit(f"K={K} must split into whole 64-rollout blocks over {world} GPUs")
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
                         num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + 2 * args.steps + 1)

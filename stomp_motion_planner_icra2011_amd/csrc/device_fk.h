@@ -118,6 +118,32 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // nearest cell round((p - origin) * (1/res)); cells with an index < 1 or >= n-1 read 0.
 // Branch-free so a lane's gathers can all be in flight together: an out-of-range lane
 // loads cell 0 and discards it.
+// C round() (halves away from zero) of u >= 0 is trunc(u) + (u - trunc(u) >= 0.5), exactly (the
+// fraction is exact in fp64); for u < 0 that gives a value <= 0, which the range check below
+// rejects just as it rejects round(u) <= 0.  No sign fix-up, no branch.
+__device__ __forceinline__ double round_nonneg(double u)
+{
+    const double t = trunc(u);
+    return t + ((u - t) >= 0.5 ? 1.0 : 0.0);
+}
+
+#ifndef SDF_LEGACY_ROUND
+__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
+{
+    const double fx = round_nonneg((p[0] - m.ox) * m.inv_res);
+    const double fy = round_nonneg((p[1] - m.oy) * m.inv_res);
+    const double fz = round_nonneg((p[2] - m.oz) * m.inv_res);
+    const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
+                    fz < (double)(m.nz - 1);
+    // the cell index in fp64 (in range every term is a small integer, so the products and sums
+    // are exact; the index fits 32 bits, checked at engine creation), selected before the one
+    // conversion: no branch; out of range the lane loads cell 0 and discards it
+    const double cell = (fx * m.ny_d + fy) * m.nz_d + fz;
+    const unsigned idx = (unsigned)(ok ? cell : 0.0);
+    const float v = m.sdf[idx];
+    return ok ? v : 0.0f;
+}
+#else
 __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
 {
     const double fx = round((p[0] - m.ox) * m.inv_res);
@@ -125,12 +151,11 @@ __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* _
     const double fz = round((p[2] - m.oz) * m.inv_res);
     const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
                     fz < (double)(m.nz - 1);
-    // in range the coordinates are small non-negative integers; the cell index fits 32 bits
-    // (checked at engine creation)
     const unsigned idx = ok ? ((unsigned)fx * (unsigned)m.ny + (unsigned)fy) * (unsigned)m.nz + (unsigned)fz : 0u;
     const float v = m.sdf[idx];
     return ok ? v : 0.0f;
 }
+#endif
 
 // StompCollisionSpace::getCollisionPointPotentialGradient (stomp_collision_space.h:193-228)
 __device__ __forceinline__ double potential(const DevSphere& s, double dist)

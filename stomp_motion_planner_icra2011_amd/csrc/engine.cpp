@@ -1088,6 +1088,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     e->terms.segs = m.segs;
     e->tq_model.segs = m.segs;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
+    m.ny_d = (double)m.ny; m.nz_d = (double)m.nz;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
     m.inv_res = 1.0 / d->grid.resolution;
     m.start = e->d_start; m.goal = e->d_goal;
@@ -1264,7 +1265,10 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
     ca.params = e->d_eval_params; ca.stride = (long long)JN; ca.num_noisy = num; ca.member = iteration_member;
     ca.state_out = e->d_eval_costs; ca.cf_out = e->d_eval_cf;
     ca.traj_out = (traj_out || e->terms_on) ? e->d_eval_traj : nullptr;
-    launch_cost(e->model, ca, e->stream);
+    {
+        Timed tm(e, T_COST);
+        launch_cost(e->model, ca, e->stream);
+    }
     if (constraints_satisfied && !e->terms_on) HIP_TRY(e, hipMemsetAsync(e->d_eval_cs, 1, (size_t)num, e->stream));
     launch_terms_for(e, ca, e->d_eval_cs);
     HIP_TRY(e, hipGetLastError());

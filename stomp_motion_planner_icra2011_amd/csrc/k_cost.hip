@@ -39,7 +39,11 @@ constexpr int kCopyBatch = 12 * 256 / kBlock;   // table-image words per lane pe
 #ifndef SPHERE_UNROLL
 #define SPHERE_UNROLL 2
 #endif
-constexpr int kSphereUnroll = SPHERE_UNROLL;   // spheres per pair lane with gathers in flight
+constexpr int kSphereUnroll = SPHERE_UNROLL;   // spheres per pair lane with gathers in flight (GATHER_ROUNDS)
+// spheres of one run a pair lane takes: run_max(N) / (BLOCK / N) <= 16 / 2 (N <= 128) or 8 / 1
+constexpr int kLaneSpheres = 8;
+static_assert(kRunMaxSmall / 2 <= kLaneSpheres && kRunMaxLarge <= kLaneSpheres && kBlock >= 256,
+              "a pair lane's spheres of one run must fit kLaneSpheres");
 }
 
 __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
@@ -329,6 +333,52 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         int next = -1;
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
         // flight) and serves spheres g, g + G, ... of the slot, kSphereUnroll gathers in flight
+#ifndef GATHER_ROUNDS
+        if (pg < G) {
+            // every sphere of the run this lane takes (at most kLaneSpheres: a run holds <= 16
+            // spheres and G >= 2 when N <= 128; <= 8 spheres and G >= 1 otherwise) is looked up
+            // with all its gathers in flight at once; the potentials and the pair list follow
+            double F[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
+            float dv[kLaneSpheres];
+#pragma unroll
+            for (int u = 0; u < kLaneSpheres; ++u) {
+                if (u * G >= ns) break;   // uniform
+                const double* pos = sph[sb + min(pg + u * G, ns - 1)].pos;
+                double x[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
+                dv[u] = sdf_distance(m, x);
+            }
+            STAMP(40 + run);
+#pragma unroll
+            for (int u = 0; u < kLaneSpheres; ++u) {
+                if (u * G >= ns) break;   // uniform
+                const int q = pg + u * G;
+                const bool in = q < ns;
+                double pot = 0.0;
+                if (in) {
+                    const DevSphere& sp = sph[sb + q];
+                    const double dd = (double)dv[u];
+                    col |= dd <= sp.radius;
+                    pot = potential(sp, dd);
+                    av[q * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                }
+                const bool nz = in && pot != 0.0;
+                const unsigned long long mask = __ballot(nz);
+                if (mask) {
+                    const int lane_id = tid & 63;
+                    const int leader = __ffsll((long long)mask) - 1;
+                    int base = 0;
+                    if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                    base = __shfl(base, leader, 64);
+                    if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
+                }
+            }
+        }
+#else
         if (pg < G) {
             double F[12];
 #pragma unroll
@@ -378,6 +428,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                 }
             }
         }
+#endif
         __syncthreads();   // pots and the non-zero list complete
         STAMP(11 + 4 * run);
         // velocities only for the listed pairs, spread densely over the block

@@ -71,6 +71,7 @@ struct DevModel {
     const float* sdf;
     int nx, ny, nz;
     double ox, oy, oz, res, inv_res;
+    double ny_d, nz_d;          // ny, nz as doubles (the fp64 cell index of sdf_distance)
     const double* start;        // [J]
     const double* goal;         // [J]
     double vel_coef[7];         // invTime * DIFF_RULES[0][k]
