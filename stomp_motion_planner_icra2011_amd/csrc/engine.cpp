@@ -167,6 +167,11 @@ struct stomp_engine {
     TermsModel tq_model{};
     double *d_tq = nullptr, *d_tq_state = nullptr;
     int wall_khz = 0;
+    // split evaluation pipeline (k_rollout prep -> k_fk -> k_pairs -> k_fold); STOMP_SPLIT=0: fused k_rollout
+    bool split = false;
+    int split_rows = 0;                // rows the split buffers hold
+    SplitBufs sbuf{};
+    double* d_traj_lim = nullptr;      // [split_rows][J][N] joint-limited trajectories
     std::shared_ptr<LocalGroup> local;   // in-process exchange group (stomp_comm_local_id), or null
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     double* d_mm_all = nullptr;          // [world][2][J][N] gathered (max, -min) of a local group
@@ -413,6 +418,38 @@ void release(stomp_engine* e)
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
 }
 
+// split-pipeline buffers for `rows` rollouts of one launch (grown on demand; hipFree waits for the device)
+int ensure_split(stomp_engine* e, int rows)
+{
+    if (rows <= e->split_rows) return 0;
+    for (void* p : {(void*)e->sbuf.frames, (void*)e->sbuf.aval, (void*)e->sbuf.colf, (void*)e->d_traj_lim}) {
+        if (!p) continue;
+        hipFree(p);
+        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), p), e->allocs.end());
+    }
+    const size_t R = (size_t)rows, N = (size_t)e->N;
+    int rc;
+    if ((rc = dev_alloc(e, &e->sbuf.frames, R * std::max(e->nslots, 1) * 12 * N))) return rc;
+    if ((rc = dev_alloc(e, &e->sbuf.aval, R * std::max(e->S, 1) * N))) return rc;
+    if ((rc = dev_alloc(e, &e->sbuf.colf, R * std::max(e->model.nruns, 1)))) return rc;
+    if ((rc = dev_alloc(e, &e->d_traj_lim, R * e->J * N))) return rc;
+    e->split_rows = rows;
+    return 0;
+}
+
+// Task::execute of a launch's rollouts: the fused k_rollout, or the split pipeline
+void launch_rollouts(stomp_engine* e, CostArgs ca)
+{
+    if (!e->split) {
+        launch_cost(e->model, ca, e->stream);
+        return;
+    }
+    const int rows = ca.num_noisy + (ca.x_params ? 1 : 0);
+    if (ensure_split(e, std::max(rows, 1))) return;   // leaves the error; the caller's hipGetLastError is clean
+    if (!ca.traj_out) ca.traj_out = e->d_traj_lim;
+    launch_split_eval(e->model, ca, e->sbuf, e->stream);
+}
+
 // the state-cost terms after the collision cost (k_terms), on the rollouts a k_rollout
 // launch with these arguments evaluated; its trajectories must have been written
 void launch_terms_for(stomp_engine* e, const CostArgs& ca, uint8_t* cs = nullptr)
@@ -448,7 +485,7 @@ void launch_noiseless(stomp_engine* e, int member)
     ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
     {
         Timed tm(e, T_NOISELESS);
-        launch_cost(e->model, ca, e->stream);
+        launch_rollouts(e, ca);
     }
     launch_terms_for(e, ca);
     track_noiseless(e, ca);
@@ -633,7 +670,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         }
         {
             Timed tm(e, T_COST);
-            launch_cost(e->model, ca, e->stream);
+            launch_rollouts(e, ca);
         }
         launch_terms_for(e, ca);
         // before this iteration's weights / update: a break decided on the previous
@@ -1100,6 +1137,20 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
     m.QT = e->d_QT;
+    {
+        // the FK program's sphere runs in order: (frame slot, first sphere, end sphere)
+        std::vector<int> runs;
+        for (const FkOp& o : e->ops)
+            if (o.sph_end > o.sph_begin) runs.insert(runs.end(), {e->sphere_slot[o.sph_begin], o.sph_begin, o.sph_end, 0});
+        m.nruns = (int)runs.size() / 4;
+        int* d_runs;
+        if (runs.empty()) runs.assign(4, 0);
+        CREATE_TRY(upload(e, &d_runs, runs.data(), runs.size()));
+        m.runs = d_runs;
+        const char* sp = std::getenv("STOMP_SPLIT");
+        e->split = sp && sp[0] == '1' && N <= 256 && e->S > 0;
+        if (e->split) CREATE_TRY(ensure_split(e, e->K_loc + 1));
+    }
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
     int pad_cf = 0;
@@ -1267,7 +1318,7 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
     ca.traj_out = (traj_out || e->terms_on) ? e->d_eval_traj : nullptr;
     {
         Timed tm(e, T_COST);
-        launch_cost(e->model, ca, e->stream);
+        launch_rollouts(e, ca);
     }
     if (constraints_satisfied && !e->terms_on) HIP_TRY(e, hipMemsetAsync(e->d_eval_cs, 1, (size_t)num, e->stream));
     launch_terms_for(e, ca, e->d_eval_cs);

@@ -78,7 +78,10 @@ struct DevModel {
     double w_obs, w_con, w_tq;
     int pad_collision;
     const double* QT;           // [J][N][N]
+    int nruns;                  // sphere runs of the FK program (ops with spheres), in sphere order
+    const int* runs;            // [nruns][4]: frame slot, first sphere, end sphere, 0
 };
+
 
 // LDS carve-up of the rollout kernel (bytes).  traj stays resident; the per-slot FK buffers
 // follow it and the noise phase's two buffers alias them (they are dead before the first
@@ -161,6 +164,7 @@ struct CostArgs {
     double* total_out;          // [num_noisy] or null
     const double* x_params;     // [J][N] or null
     int x_member;
+    int prep_only;              // 1: noise phase + handleJointLimits + traj_out / x_traj only (split pipeline)
     int pre_rows;               // > 0: blocks after the rollouts make k_pregen's rows of pre_next (the
     NoiseArgs pre_next;         // next iteration) at low priority in the same dispatch
     double* x_state;
@@ -168,6 +172,16 @@ struct CostArgs {
     double* x_traj;
     double* x_total;
 };
+
+// Buffers of the split evaluation pipeline (k_rollout prep_only -> k_fk -> k_pairs -> k_fold),
+// rows = the launch's noisy rollouts and the noiseless one (row num_noisy)
+struct SplitBufs {
+    double* frames;             // [rows][nslots][12][N] FK frame of every sphere-carrying segment
+    double* aval;               // [rows][S][N] a = pot * |v| (stomp_optimizer.cpp:1100-1105)
+    int* colf;                  // [rows][nruns] any sphere of the run in collision
+};
+void launch_split_eval(const DevModel& m, const CostArgs& a, const SplitBufs& b, hipStream_t s);
+size_t split_pairs_lds_bytes(const DevModel& m);
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
 
