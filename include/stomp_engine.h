@@ -23,6 +23,9 @@
  *                            StompCollisionSpace::setStartState + PropagationDistanceField
  *                            produce (stomp_collision_space.cpp:154-197), for box and
  *                            z-cylinder obstacles, directly in device memory
+ *   stomp_sdf_build_objects  the same fill by the reference's own rules: posed boxes and
+ *                            cylinders sampled on its lattice, robot bodies, collision-map
+ *                            points (stomp_collision_space.cpp:199-297, 564-650)
  *
  * Conventions: plain pointers and sizes only; host buffers are caller-owned and
  * read/written during the call; device buffers are engine-owned.  Trajectories
@@ -258,6 +261,43 @@ int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
 int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
                     double max_expansion, const double* boxes, int32_t n_boxes, const double* cylinders,
                     int32_t n_cylinders, float* out_device, void* stream);
+
+/* An object of the collision space.  Environment objects are sampled as
+ * StompCollisionSpace::addCollisionObjectsToPoints does (stomp_collision_space.cpp:199-297):
+ *   STOMP_SHAPE_BOX       dims = (dx, dy, dz)
+ *   STOMP_SHAPE_CYLINDER  dims = (radius, length, -), axis = the pose's z
+ * on the running-sum lattice xlow, xlow + res, ... (x <= xlow + dim + res), each point p
+ * mapped through Frame(Rotation::Quaternion(orientation), position) as position - p.
+ * Robot bodies (getVoxelsInBody, :592-650; the links addAllBodiesButExcludeLinksToPoints keeps,
+ * :564-590, with the caller's padding/scale folded into dims):
+ *   STOMP_BODY_SPHERE     dims = (radius, -, -)
+ *   STOMP_BODY_BOX        dims = (dx, dy, dz)
+ *   STOMP_BODY_CYLINDER   dims = (radius, length, -)
+ * on the lattice position + g * res around the bounding sphere, kept where the body contains
+ * the point (the reference's ray-crossing parity for these convex primitives). */
+#define STOMP_SHAPE_BOX 0
+#define STOMP_SHAPE_CYLINDER 1
+#define STOMP_BODY_SPHERE 2
+#define STOMP_BODY_BOX 3
+#define STOMP_BODY_CYLINDER 4
+typedef struct stomp_shape {
+    int32_t type;
+    double position[3];
+    double orientation[4];      /* quaternion (x, y, z, w), geometry_msgs::Pose order */
+    double dims[3];
+} stomp_shape;
+
+/* The reference's distance-field fill (StompCollisionSpace::setStartState,
+ * stomp_collision_space.cpp:154-197) on the device: every object's points and the
+ * collision-map points (points: n_points x 3, the "points" namespace, :205-211) mark the cell
+ * round((p - origin) * (1/res)) when it lies in the grid (PropagationDistanceField::
+ * addPointsToField); value = sqrt(min(d2, cap^2)) * res with cap = ceil(max_expansion/res)
+ * (<= 255) and d2 the integer squared cell distance to the nearest marked cell.
+ * marked (may be NULL): points that landed inside the grid.  Meshes are not supported. */
+int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
+                            double max_expansion, const stomp_shape* shapes, int32_t n_shapes,
+                            const double* points, int64_t n_points, float* out_device, int64_t* marked,
+                            void* stream);
 
 /* The differentiation stencils the engine is built on (DIFF_RULES of stomp_utils.h:49-56:
  * velocity, acceleration, jerk; 3 x 7 doubles, row-major).  Host only, no device needed. */

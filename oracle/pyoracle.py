@@ -114,8 +114,51 @@ def lib():
         l.so_atan2.argtypes = [C.c_double, C.c_double]
         l.so_asin.restype = C.c_double
         l.so_asin.argtypes = [C.c_double]
+        l.so_sdf_build_objects.restype = C.c_longlong
+        l.so_sdf_build_objects.argtypes = [C.c_int, C.c_int, C.c_int, dp, C.c_double, C.c_double,
+                                           C.POINTER(so_shape), C.c_int, dp, C.c_longlong,
+                                           C.POINTER(C.c_ubyte), C.POINTER(C.c_float)]
+        l.so_sdf_from_occupancy.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                            C.POINTER(C.c_ubyte), C.POINTER(C.c_float)]
         _lib = l
     return _lib
+
+
+class so_shape(C.Structure):
+    _fields_ = [("type", C.c_int), ("position", C.c_double * 3), ("orientation", C.c_double * 4),
+                ("dims", C.c_double * 3)]
+
+
+def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
+    """so_sdf_build_objects (oracle/sdf_oracle.c) for problem.Grid `grid`: (field n^3 fp32 or None,
+    marks n^3 uint8, number of points marked)."""
+    n = grid.n
+    arr = (so_shape * max(len(objects), 1))()
+    for i, o in enumerate(objects):
+        arr[i].type = int(o.type)
+        arr[i].position[:] = [float(v) for v in o.position]
+        arr[i].orientation[:] = [float(v) for v in o.orientation]
+        d = list(o.dims) + [0.0] * (3 - len(o.dims))
+        arr[i].dims[:] = [float(v) for v in d[:3]]
+    pts = np.ascontiguousarray(points if points is not None else np.zeros((0, 3)), np.float64).reshape(-1, 3)
+    occ = np.zeros((n, n, n), np.uint8)
+    field = np.zeros((n, n, n), np.float32) if with_field else None
+    origin = np.array(grid.origin, np.float64)
+    marked = lib().so_sdf_build_objects(
+        n, n, n, _dp(origin), grid.resolution, grid.max_expansion, arr, len(objects),
+        _dp(pts if pts.size else np.zeros(3)), len(pts), occ.ctypes.data_as(C.POINTER(C.c_ubyte)),
+        field.ctypes.data_as(C.POINTER(C.c_float)) if field is not None else None)
+    if marked < 0:
+        raise ValueError("so_sdf_build_objects: invalid input")
+    return field, occ, int(marked)
+
+
+def sdf_from_occupancy(occ: np.ndarray, resolution: float, max_expansion: float) -> np.ndarray:
+    occ = np.ascontiguousarray(occ, np.uint8)
+    out = np.zeros(occ.shape, np.float32)
+    lib().so_sdf_from_occupancy(*occ.shape, resolution, max_expansion, occ.ctypes.data_as(C.POINTER(C.c_ubyte)),
+                                out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out
 
 
 def _dp(a: np.ndarray):

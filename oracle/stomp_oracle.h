@@ -196,6 +196,25 @@ int so_sphere_positions(const so_problem* p, const double* q, double* out);
 double so_sdf_distance(const so_problem* p, double x, double y, double z);
 int so_potential(const so_problem* p, int sphere, const double* pos, double* potential);
 
+/* Collision-space voxeliser (oracle/sdf_oracle.c): the shapes of
+ * StompCollisionSpace::addCollisionObjectsToPoints (stomp_collision_space.cpp:199-297) and
+ * the robot bodies of getVoxelsInBody (:592-650), marked into a grid and turned into the
+ * capped, quantised EDT.  Types as stomp_engine.h STOMP_SHAPE_* / STOMP_BODY_*. */
+typedef struct {
+    int type;
+    double position[3];
+    double orientation[4];   /* quaternion x, y, z, w */
+    double dims[3];
+} so_shape;
+/* occ (nx*ny*nz bytes, may be NULL) receives the marked cells; sdf (floats, may be NULL) the
+ * field sqrt(min(d2, cap^2)) * res.  Returns the number of points marked (inside the grid). */
+long long so_sdf_build_objects(int nx, int ny, int nz, const double* origin, double res, double max_expansion,
+                               const so_shape* shapes, int n_shapes, const double* points, long long n_points,
+                               unsigned char* occ, float* sdf);
+/* capped EDT of an occupancy grid alone (the second half of so_sdf_build_objects) */
+void so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,
+                           float* sdf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1763,6 +1763,149 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
     return 0;
 }
 
+// StompCollisionSpace::setStartState's fill (stomp_collision_space.cpp:154-297, 564-650): the
+// per-object lattice is set up here (the environment objects' coordinate lists by the reference's
+// own running-sum loops), the marking and the EDT run on the device (k_sdf.hip)
+int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* origin, double res,
+                            double max_expansion, const stomp_shape* shapes, int32_t n_shapes, const double* points,
+                            int64_t n_points, float* out, int64_t* marked, void* stream)
+{
+    if (nx <= 0 || ny <= 0 || nz <= 0 || !(res > 0) || !out || !origin || n_shapes < 0 || n_points < 0 ||
+        (n_shapes > 0 && !shapes) || (n_points > 0 && !points))
+        return fail(nullptr, STOMP_E_INVALID, "invalid grid or object list");
+    const double capd = std::ceil(max_expansion / res);
+    if (!(capd >= 0) || capd > 255) return fail(nullptr, STOMP_E_UNSUPPORTED, "max_expansion / resolution above 255 cells");
+    const int cap = (int)capd;
+    std::vector<double> axes;
+    std::vector<SdfLatticeJob> jobs;
+    const long long kMaxLattice = 1LL << 31;
+    for (int s = 0; s < n_shapes; ++s) {
+        const stomp_shape& sh = shapes[s];
+        SdfLatticeJob j{};
+        j.type = sh.type;
+        j.res = res;
+        for (int a = 0; a < 3; ++a) {
+            j.pos[a] = sh.position[a];
+            j.dims[a] = sh.dims[a];
+        }
+        const double qx = sh.orientation[0], qy = sh.orientation[1], qz = sh.orientation[2], qw = sh.orientation[3];
+        if (sh.type == STOMP_SHAPE_BOX || sh.type == STOMP_SHAPE_CYLINDER) {
+            // KDL::Rotation::Quaternion(x, y, z, w) (:243-246)
+            const double x2 = qx * qx, y2 = qy * qy, z2 = qz * qz, w2 = qw * qw;
+            const double R[9] = {w2 + x2 - y2 - z2, 2 * qx * qy - 2 * qw * qz, 2 * qx * qz + 2 * qw * qy,
+                                 2 * qx * qy + 2 * qw * qz, w2 - x2 + y2 - z2, 2 * qy * qz - 2 * qw * qx,
+                                 2 * qx * qz - 2 * qw * qy, 2 * qy * qz + 2 * qw * qx, w2 - x2 - y2 + z2};
+            std::memcpy(j.R, R, sizeof R);
+            const bool cyl = sh.type == STOMP_SHAPE_CYLINDER;
+            const double* p = sh.position;
+            const double* d = sh.dims;
+            const double low[3] = {cyl ? p[0] - d[0] : p[0] - d[0] / 2.0, cyl ? p[1] - d[0] : p[1] - d[1] / 2.0,
+                                   cyl ? p[2] - d[1] / 2.0 : p[2] - d[2] / 2.0};
+            const double ext[3] = {cyl ? d[0] * 2.0 : d[0], cyl ? d[0] * 2.0 : d[1], cyl ? d[1] : d[2]};
+            long long npts = 1;
+            for (int a = 0; a < 3; ++a) {
+                j.off[a] = (int)axes.size();
+                // for (double x = xlow; x <= xlow + dim + resolution_; x += resolution_) (:255-257, 283-285)
+                for (double x = low[a]; x <= low[a] + ext[a] + res; x += res) {
+                    axes.push_back(x);
+                    if ((long long)axes.size() - j.off[a] > kMaxLattice)
+                        return fail(nullptr, STOMP_E_INVALID, "object %d: lattice too large", s);
+                }
+                j.n[a] = (int)axes.size() - j.off[a];
+                npts *= j.n[a];
+            }
+            if (npts > kMaxLattice) return fail(nullptr, STOMP_E_INVALID, "object %d: lattice too large", s);
+        } else if (sh.type >= STOMP_BODY_SPHERE && sh.type <= STOMP_BODY_CYLINDER) {
+            // btMatrix3x3::setRotation (bodies::Body::setPose)
+            const double dq = qx * qx + qy * qy + qz * qz + qw * qw;
+            const double sc = 2.0 / dq;
+            const double xs = qx * sc, ys = qy * sc, zs = qz * sc;
+            const double wx = qw * xs, wy = qw * ys, wz = qw * zs;
+            const double xx = qx * xs, xy = qx * ys, xz = qx * zs;
+            const double yy = qy * ys, yz = qy * zs, zz = qz * zs;
+            const double B[9] = {1.0 - (yy + zz), xy - wz, xz + wy, xy + wz, 1.0 - (xx + zz), yz - wx,
+                                 xz - wy, yz + wx, 1.0 - (xx + yy)};
+            std::memcpy(j.R, B, sizeof B);
+            const double* d = sh.dims;
+            double r;   // bodies::*::computeBoundingSphere
+            if (sh.type == STOMP_BODY_SPHERE) {
+                r = d[0];
+            } else if (sh.type == STOMP_BODY_BOX) {
+                const double a = d[0] / 2.0, b = d[1] / 2.0, c = d[2] / 2.0;
+                r = std::sqrt(a * a + b * b + c * c);
+            } else {
+                const double h = d[1] / 2.0;
+                r = std::sqrt(d[0] * d[0] + h * h);
+            }
+            long long npts = 1;
+            for (int a = 0; a < 3; ++a) {
+                const double c = sh.position[a];
+                const double lo = ((c - r) - c) * (1.0 / res), hi = ((c + r) - c) * (1.0 / res);
+                if (!(std::fabs(lo) < 1e9 && std::fabs(hi) < 1e9))
+                    return fail(nullptr, STOMP_E_INVALID, "body %d: lattice too large", s);
+                j.lo[a] = (int)lo;   // worldToGrid truncates (stomp_collision_space.h:230-234)
+                j.n[a] = (int)hi - j.lo[a] + 1;
+                if (j.n[a] < 0) j.n[a] = 0;
+                npts *= j.n[a];
+            }
+            if (npts > kMaxLattice) return fail(nullptr, STOMP_E_INVALID, "body %d: lattice too large", s);
+        } else {
+            return fail(nullptr, STOMP_E_INVALID, "object %d: unknown type %d", s, sh.type);
+        }
+        jobs.push_back(j);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const size_t cells = (size_t)nx * ny * nz;
+    unsigned char* occ = nullptr;
+    unsigned short *a = nullptr, *b = nullptr;
+    double *d_axes = nullptr, *d_pts = nullptr;
+    unsigned long long* d_marked = nullptr;
+    auto cleanup = [&]() {
+        if (occ) hipFree(occ);
+        if (a) hipFree(a);
+        if (b) hipFree(b);
+        if (d_axes) hipFree(d_axes);
+        if (d_pts) hipFree(d_pts);
+        if (d_marked) hipFree(d_marked);
+    };
+    if (hipMalloc(&occ, cells) != hipSuccess || hipMalloc(&a, cells * 2) != hipSuccess ||
+        hipMalloc(&b, cells * 2) != hipSuccess || hipMalloc(&d_marked, sizeof(unsigned long long)) != hipSuccess ||
+        (!axes.empty() && hipMalloc(&d_axes, axes.size() * sizeof(double)) != hipSuccess) ||
+        (n_points > 0 && hipMalloc(&d_pts, (size_t)n_points * 3 * sizeof(double)) != hipSuccess)) {
+        cleanup();
+        return fail(nullptr, STOMP_E_DEVICE, "sdf build: hipMalloc");
+    }
+    hipError_t err = hipMemsetAsync(occ, 0, cells, st);
+    if (err == hipSuccess) err = hipMemsetAsync(d_marked, 0, sizeof(unsigned long long), st);
+    if (err == hipSuccess && d_axes)
+        err = hipMemcpyAsync(d_axes, axes.data(), axes.size() * sizeof(double), hipMemcpyHostToDevice, st);
+    if (err == hipSuccess && d_pts)
+        err = hipMemcpyAsync(d_pts, points, (size_t)n_points * 3 * sizeof(double), hipMemcpyHostToDevice, st);
+    if (err != hipSuccess) {
+        cleanup();
+        return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(err));
+    }
+    SdfMarkArgs g{};
+    g.n[0] = nx;
+    g.n[1] = ny;
+    g.n[2] = nz;
+    for (int k = 0; k < 3; ++k) g.o[k] = origin[k];
+    g.inv_res = 1.0 / res;
+    g.occ = occ;
+    g.marked = d_marked;
+    launch_mark_points(d_pts, n_points, g, st);
+    for (const SdfLatticeJob& j : jobs) launch_mark_lattice(j, d_axes, g, st);
+    launch_edt(nx, ny, nz, cap, occ, a, b, out, res, st);
+    unsigned long long nm = 0;
+    err = hipGetLastError();
+    if (err == hipSuccess) err = hipMemcpyAsync(&nm, d_marked, sizeof nm, hipMemcpyDeviceToHost, st);
+    if (err == hipSuccess) err = hipStreamSynchronize(st);
+    cleanup();
+    if (err != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(err));
+    if (marked) *marked = (int64_t)nm;
+    return 0;
+}
+
 int stomp_diff_rules(double* out)
 {
     if (!out) return fail(nullptr, STOMP_E_INVALID, "null argument");

@@ -309,4 +309,28 @@ void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* b
                       int nb, const long long* cyl_d2 /*nc x nx x ny*/, const int* cyl_z /*nc x 2*/, int nc,
                       float* out, hipStream_t s);
 
+// the reference's object voxeliser (k_sdf.hip); shape types as STOMP_SHAPE_* / STOMP_BODY_*
+constexpr int kShapeBox = 0, kShapeCylinder = 1, kBodySphere = 2, kBodyBox = 3, kBodyCylinder = 4;
+struct SdfMarkArgs {
+    int n[3];
+    double o[3];
+    double inv_res;              // 1.0 / res (VoxelGrid oo_resolution)
+    unsigned char* occ;          // nx*ny*nz marks
+    unsigned long long* marked;  // points that landed inside the grid
+};
+struct SdfLatticeJob {
+    int type;
+    int n[3];                    // lattice points per axis
+    int off[3];                  // environment objects: offsets of the axis coordinate lists
+    int lo[3];                   // robot bodies: first lattice index per axis
+    double pos[3];
+    double R[9];                 // KDL Rotation::Quaternion (objects) / btMatrix3x3 basis (bodies)
+    double dims[3];
+    double res;
+};
+void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMarkArgs& g, hipStream_t s);
+void launch_mark_points(const double* pts, long long np, const SdfMarkArgs& g, hipStream_t s);
+void launch_edt(int nx, int ny, int nz, int cap, const unsigned char* occ, unsigned short* a, unsigned short* b,
+                float* field, double res, hipStream_t s);
+
 }  // namespace stomp

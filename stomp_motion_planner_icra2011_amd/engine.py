@@ -26,6 +26,11 @@ class stomp_sphere(C.Structure):
     _fields_ = [("segment", C.c_int32), ("radius", C.c_double), ("clearance", C.c_double), ("pos", C.c_double * 3)]
 
 
+class stomp_shape(C.Structure):
+    _fields_ = [("type", C.c_int32), ("position", C.c_double * 3), ("orientation", C.c_double * 4),
+                ("dims", C.c_double * 3)]
+
+
 class stomp_joint(C.Structure):
     _fields_ = [("has_limits", C.c_int32), ("min", C.c_double), ("max", C.c_double), ("joint_cost", C.c_double)]
 
@@ -84,7 +89,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
             "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id",
             "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
-            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts"]
+            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_sdf_build_objects"]
 
 _lib = None
 
@@ -129,6 +134,9 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_local_rollouts.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     l.stomp_sdf_build.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double, dp, C.c_int32, dp,
                                   C.c_int32, C.c_void_p, C.c_void_p]
+    l.stomp_sdf_build_objects.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double,
+                                          C.POINTER(stomp_shape), C.c_int32, dp, C.c_int64, C.c_void_p,
+                                          C.POINTER(C.c_int64), C.c_void_p]
     l.stomp_comm_unique_id.argtypes = [C.c_void_p]
     l.stomp_comm_local_id.argtypes = [C.c_int32, C.c_void_p]
     l.stomp_device_alloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
@@ -165,6 +173,32 @@ def sdf_build_device(problem, device_tensor_ptr: int, stream: int = 0):
     _check(l.stomp_sdf_build(g.n, g.n, g.n, _dp(origin), g.resolution, g.max_expansion, _dp(boxes),
                              len(problem.boxes), _dp(cyl), len(problem.cylinders), C.c_void_p(device_tensor_ptr),
                              C.c_void_p(stream)))
+
+
+def shape_array(objects):
+    """problem.SceneObject list -> stomp_shape[] (ctypes array; length >= 1)."""
+    arr = (stomp_shape * max(len(objects), 1))()
+    for i, o in enumerate(objects):
+        arr[i].type = int(o.type)
+        arr[i].position[:] = [float(v) for v in o.position]
+        arr[i].orientation[:] = [float(v) for v in o.orientation]
+        d = list(o.dims) + [0.0] * (3 - len(o.dims))
+        arr[i].dims[:] = [float(v) for v in d[:3]]
+    return arr
+
+
+def sdf_build_objects_device(grid, objects, device_ptr: int, points=None, stream: int = 0) -> int:
+    """The reference's distance-field fill (stomp_sdf_build_objects) of problem.Grid `grid` from
+    collision objects (problem.SceneObject) and collision-map points (P x 3) into a device buffer
+    of n^3 floats.  Returns the number of points that landed in the grid."""
+    l = load_library()
+    origin = np.array(grid.origin, np.float64)
+    pts = np.ascontiguousarray(points if points is not None else np.zeros((0, 3)), np.float64).reshape(-1, 3)
+    marked = C.c_int64(0)
+    _check(l.stomp_sdf_build_objects(grid.n, grid.n, grid.n, _dp(origin), grid.resolution, grid.max_expansion,
+                                     shape_array(objects), len(objects), _dp(pts if pts.size else np.zeros(3)),
+                                     len(pts), C.c_void_p(device_ptr), C.byref(marked), C.c_void_p(stream)))
+    return marked.value
 
 
 class Engine:

@@ -243,6 +243,38 @@ def shelf_scene(with_pole: bool = True):
     return boxes, cyls
 
 
+# collision-space objects as the reference's voxeliser takes them (stomp_engine.h STOMP_SHAPE_* /
+# STOMP_BODY_*; stomp_collision_space.cpp:199-297, 592-650)
+SHAPE_BOX, SHAPE_CYLINDER, BODY_SPHERE, BODY_BOX, BODY_CYLINDER = 0, 1, 2, 3, 4
+
+
+@dataclasses.dataclass
+class SceneObject:
+    type: int
+    position: Sequence[float]
+    orientation: Sequence[float] = (0.0, 0.0, 0.0, 1.0)   # quaternion x, y, z, w
+    dims: Sequence[float] = (0.0, 0.0, 0.0)
+
+
+def quaternion_from_rpy(roll: float, pitch: float, yaw: float):
+    """btQuaternion::setRPY, as test_collision_world.cpp:180-185 turns a scene file's
+    orientation [roll, pitch, yaw] into the object's pose quaternion (x, y, z, w)."""
+    hy, hp, hr = yaw * 0.5, pitch * 0.5, roll * 0.5
+    cy, sy, cp, sp, cr, sr = math.cos(hy), math.sin(hy), math.cos(hp), math.sin(hp), math.cos(hr), math.sin(hr)
+    return (sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+            cr * cp * cy + sr * sp * sy)
+
+
+def shelf_objects(with_pole: bool = True) -> List[SceneObject]:
+    """The shelf + pole scene (shelf_scene) as collision objects with the scene files' poses
+    (environment_shelf.yaml:4-64, environment_pole.yaml:4-10; orientation [0, 0, 0])."""
+    boxes, cyls = shelf_scene(with_pole)
+    q = quaternion_from_rpy(0.0, 0.0, 0.0)
+    out = [SceneObject(SHAPE_BOX, tuple(b.center), q, tuple(b.dims)) for b in boxes]
+    out += [SceneObject(SHAPE_CYLINDER, tuple(c.center), q, (c.radius, c.length, 0.0)) for c in cyls]
+    return out
+
+
 @dataclasses.dataclass
 class Grid:
     n: int                    # cells per axis (cube)

@@ -1,0 +1,90 @@
+"""GPU: the reference's distance-field fill on the device (stomp_sdf_build_objects, k_sdf.hip)
+against oracle/sdf_oracle.c, bit for bit (tests/test_sdf_objects.py pins the oracle to the
+reference's loops and to a brute-force EDT).  Paths relative to /root/reference/stomp_motion_planner/:
+stomp_collision_space.cpp:154-297 (objects, points), :564-650 (robot bodies)."""
+import numpy as np
+import pytest
+
+from stomp_motion_planner_icra2011_amd import problem as pb
+from stomp_motion_planner_icra2011_amd import engine as eng
+from oracle import pyoracle as po
+
+from tests.test_sdf_objects import mixed_scene, small_grid
+
+pytestmark = pytest.mark.gpu
+
+
+def device_field(grid, objs, pts=None):
+    n = grid.n
+    buf = eng.DeviceBuffer(4 * n ** 3)
+    marked = eng.sdf_build_objects_device(grid, objs, buf.ptr, pts)
+    return buf.to_numpy(np.float32, (n, n, n)), marked
+
+
+@pytest.mark.parametrize("n", [32, 64, 128])
+def test_mixed_scene_bitwise(n):
+    grid = small_grid(n)
+    objs, pts = mixed_scene()
+    want, _, count = po.sdf_build_objects(grid, objs, pts)
+    got, marked = device_field(grid, objs, pts)
+    assert marked == count
+    np.testing.assert_array_equal(got, want)
+
+
+def test_shelf_scene_256_bitwise():
+    grid = pb.default_grid(256)
+    objs = pb.shelf_objects()
+    q = pb.quaternion_from_rpy
+    objs.append(pb.SceneObject(pb.SHAPE_BOX, (0.4, 0.5, 0.6), q(0.2, 0.4, -0.9), (0.3, 0.05, 0.5)))
+    want, _, count = po.sdf_build_objects(grid, objs)
+    got, marked = device_field(grid, objs)
+    assert marked == count
+    np.testing.assert_array_equal(got, want)
+
+
+def test_shelf_scene_512_marks_and_rim():
+    """cfg4's 512^3 grid (the oracle's EDT is too slow there): the cells the device field puts at
+    distance 0 are exactly the oracle's marks, and the capped value holds far from every mark."""
+    grid = pb.default_grid(512)
+    objs = pb.shelf_objects()
+    _, occ, count = po.sdf_build_objects(grid, objs, with_field=False)
+    got, marked = device_field(grid, objs)
+    assert marked == count
+    np.testing.assert_array_equal(got == 0.0, occ > 0)
+    cap = int(np.ceil(grid.max_expansion / grid.resolution))
+    assert got.max() == np.float32(np.sqrt(float(cap * cap)) * grid.resolution)
+    # a slab well inside the field, checked against the oracle EDT of the marks it can see
+    sub = occ[200:300, 200:300, 100:160]
+    ref = po.sdf_from_occupancy(np.ascontiguousarray(occ[200 - cap:300 + cap, 200 - cap:300 + cap, 100 - cap:160 + cap]),
+                                grid.resolution, grid.max_expansion)
+    np.testing.assert_array_equal(got[200:300, 200:300, 100:160], ref[cap:-cap, cap:-cap, cap:-cap])
+    assert sub.any()
+
+
+def test_engine_iterations_on_lattice_field():
+    """The engine on a device-built reference-rule field, against the oracle on its own build of
+    the same field: 3 iterations bit for bit."""
+    p = pb.make_problem(grid_n=128, num_rollouts=16, num_reused_rollouts=0, build_grid=False)
+    objs = pb.shelf_objects()
+    p.sdf, _, _ = po.sdf_build_objects(p.grid, objs)
+    n = p.grid.n
+    buf = eng.DeviceBuffer(4 * n ** 3)
+    eng.sdf_build_objects_device(p.grid, objs, buf.ptr)
+    e = eng.Engine(p, sdf_device_ptr=buf.ptr)
+    o = po.Oracle(p)
+    for it in (1, 2, 3):
+        ec, ecf = e.iterate(it)
+        oc, ocf = o.iterate(it)
+        assert ec == oc and ecf == ocf
+    np.testing.assert_array_equal(e.theta(), o.theta())
+    np.testing.assert_array_equal(e.rollouts("state_costs"), o.rollouts("state_costs"))
+
+
+def test_invalid_inputs_refused():
+    grid = small_grid(16)
+    buf = eng.DeviceBuffer(4 * 16 ** 3)
+    with pytest.raises(RuntimeError):
+        eng.sdf_build_objects_device(grid, [pb.SceneObject(9, (0, 0, 0))], buf.ptr)
+    big = pb.Grid(16, grid.origin, 0.001, 1.0)   # cap = 1000 cells > 255
+    with pytest.raises(RuntimeError):
+        eng.sdf_build_objects_device(big, [], buf.ptr)
