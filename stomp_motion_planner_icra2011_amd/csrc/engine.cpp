@@ -121,6 +121,10 @@ struct stomp_engine {
     double *d_last_traj = nullptr, *d_best_traj = nullptr, *d_total = nullptr;
     double *d_tmp_params = nullptr, *d_tmp_state = nullptr, *d_pad_pos = nullptr, *d_start = nullptr,
            *d_goal = nullptr;
+    // sharded reuse (world > 1, K_r > 0): per-rank totals, all totals, the extra's total, the
+    // chosen rows' slots [Kr][J N + N] and their all-gather [world][Kr][J N + N], the ranking
+    double *d_tot_loc = nullptr, *d_tot_all = nullptr, *d_tot_x = nullptr, *d_slot = nullptr, *d_slot_all = nullptr;
+    int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
     float* d_sdf = nullptr;
     int* d_pad_cf = nullptr;
@@ -598,21 +602,39 @@ NoiseArgs pregen_args(const stomp_engine* e, int it)
 
 // generateRollouts bookkeeping (policy_improvement.cpp:167-225): the first call generates all K;
 // later ones rank the K previous rollouts and the extra (noiseless) one, keep the best K_r in rows
-// K_gen.. with their noise re-based on the current theta, and generate the rest
-void begin_generate(stomp_engine* e)
+// K_gen.. with their noise re-based on the current theta, and generate the rest.  With the rows
+// sharded over ranks the ranking runs on all-gathered totals and the chosen rows travel in slots
+// (k_misc.hip), so every rank ends with exactly its rows of the single-device result.
+int begin_generate(stomp_engine* e)
 {
     e->K_gen = e->K - e->Kr;
     if (!e->reused_next) {
         e->K_gen = e->K;
         if (e->Kr > 0) e->reused_next = true;
-    } else {
-        flush_noiseless(e);
-        Timed tm(e, T_REUSE);
-        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, e->extra_added ? 1 : 0, e->d_params, e->d_noise, e->d_state,
-                     e->d_control, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params,
-                     e->d_tmp_state, e->d_stop, e->stream);
-        e->extra_added = false;
+        return 0;
     }
+    flush_noiseless(e);
+    Timed tm(e, T_REUSE);
+    const int with_extra = e->extra_added ? 1 : 0;
+    e->extra_added = false;
+    if (e->world == 1) {
+        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params, e->d_noise, e->d_state, e->d_control,
+                     e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params, e->d_tmp_state,
+                     e->d_stop, e->stream);
+        return 0;
+    }
+    const size_t slot = (size_t)e->Kr * ((size_t)e->J * e->N + e->N);
+    launch_reuse_totals(e->K_loc, e->J, e->N, e->d_state, e->d_control, e->d_x_state, e->d_x_control, e->d_tot_loc,
+                        e->d_tot_x, e->d_stop, e->stream);
+    int rc = exchange_gather(e, e->d_tot_loc, e->d_tot_all, (size_t)e->K_loc);
+    if (rc) return rc;
+    launch_reuse_select(e->K, e->Kr, with_extra, e->d_tot_all, e->d_tot_x, e->d_sel, e->d_stop, e->stream);
+    launch_reuse_pack(e->Kr, e->J, e->N, e->first, e->K_loc, e->d_sel, e->d_params, e->d_state, e->d_slot, e->d_stop,
+                      e->stream);
+    if ((rc = exchange_gather(e, e->d_slot, e->d_slot_all, slot))) return rc;
+    launch_reuse_unpack(e->Kr, e->K_gen, e->J, e->N, e->first, e->K_loc, e->d_sel, e->d_slot_all, e->d_x_params,
+                        e->d_x_state, e->d_theta, e->d_params, e->d_noise, e->d_state, e->d_stop, e->stream);
+    return 0;
 }
 
 // One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
@@ -624,7 +646,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     NoiseArgs na = noise_args(e, it);
     if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
 
-    begin_generate(e);
+    {
+        int rc = begin_generate(e);
+        if (rc) return rc;
+    }
     na.K_gen_global = e->K_gen;
     // generated rows [0, g1 - g0) of this shard: their noise is made by the rollout kernel
     // itself (fused), k_noise only projects and prices the reused rows after them
@@ -794,8 +819,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         if (!d->comm_id) return fail(nullptr, STOMP_E_INVALID, "world_size > 1 needs a comm_id");
         if (d->rank < 0 || d->rank >= world)
             return fail(nullptr, STOMP_E_INVALID, "rank %d outside [0, world_size %d)", d->rank, world);
-        if (d->num_reused_rollouts > 0)
-            return fail(nullptr, STOMP_E_UNSUPPORTED, "rollout reuse is single-device only");
         if (d->num_rollouts % (world * kSumBlock) != 0)
             return fail(nullptr, STOMP_E_INVALID, "num_rollouts must be a multiple of 64 * world_size");
 #ifndef STOMP_WITH_RCCL
@@ -973,6 +996,15 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
     CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
     CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
+    if (e->world > 1 && e->Kr > 0) {
+        const size_t slot = (size_t)e->Kr * ((size_t)J * N + N);
+        CREATE_TRY(dev_alloc(e, &e->d_tot_loc, (size_t)e->K_loc));
+        CREATE_TRY(dev_alloc(e, &e->d_tot_all, (size_t)e->K));
+        CREATE_TRY(dev_alloc(e, &e->d_tot_x, 1));
+        CREATE_TRY(dev_alloc(e, &e->d_sel, (size_t)e->Kr));
+        CREATE_TRY(dev_alloc(e, &e->d_slot, slot));
+        CREATE_TRY(dev_alloc(e, &e->d_slot_all, slot * e->world));
+    }
     if (hipHostMalloc((void**)&e->h_total, sizeof(double)) != hipSuccess ||
         hipHostMalloc((void**)&e->h_cf, 16) != hipSuccess)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc failed"));
@@ -1450,7 +1482,7 @@ int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* nois
     if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
     if (!noise_stddev) return fail(e, STOMP_E_INVALID, "null noise_stddev");
     flush_noiseless(e);
-    begin_generate(e);
+    if (int rc = begin_generate(e)) return rc;
     NoiseArgs na = noise_args(e, iteration);
     for (int d = 0; d < e->J; ++d) na.sigma.v[d] = noise_stddev[d];   // generateRollouts(noise_stddev)
     na.stop = nullptr;

@@ -2,6 +2,8 @@
 // distance-field construction.
 #include "device_fk.h"
 
+#include <algorithm>
+
 #include <map>
 #include <mutex>
 #include <utility>
@@ -153,6 +155,126 @@ void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double
     const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
     hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, params, noise, state,
                        control, x_params, x_state, x_control, theta, tmp_params, tmp_state, stop);
+}
+
+// ---- the same reuse step with the K rows sharded over ranks: every rank prices its
+// own rows (Rollout::getCost, policy_improvement.cpp:149-156), the totals are all-gathered, every
+// rank ranks all K + 1 candidates identically, the owners pack the chosen rows into slot r of a
+// [Kr][J N + N] buffer, the slots are all-gathered and every rank unpacks the reused rows it owns
+// (rows K_gen + r, noise re-based on theta, :214-223).  Same ranking, same row order, so the result
+// is the single-device one bit for bit.
+__device__ __forceinline__ double rollout_total(const double* st, const double* ct, int J, int N)
+{
+    double s = st[0];
+    for (int t = 1; t < N; ++t) s += st[t];
+    for (int d = 0; d < J; ++d) {
+        double x = ct[(size_t)d * N];
+        for (int t = 1; t < N; ++t) x += ct[(size_t)d * N + t];
+        s += x;
+    }
+    return s != s ? __builtin_inf() : s;   // NaN ranks last (as k_reuse)
+}
+
+__global__ __launch_bounds__(256) void k_reuse_totals(int K_loc, int J, int N, const double* state,
+                                                      const double* control, const double* x_state,
+                                                      const double* x_control, double* tot_loc, double* tot_x,
+                                                      const int* stop)
+{
+    if (stop && *stop) return;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const size_t JN = (size_t)J * N;
+    if (c < K_loc) tot_loc[c] = rollout_total(state + (size_t)c * N, control + (size_t)c * JN, J, N);
+    else if (c == K_loc) *tot_x = rollout_total(x_state, x_control, J, N);
+}
+
+__global__ __launch_bounds__(256) void k_reuse_select(int K, int Kr, int with_extra, const double* tot_all,
+                                                      const double* tot_x, int* sel, const int* stop)
+{
+    if (stop && *stop) return;
+    const int n = K + with_extra;
+    for (int c = threadIdx.x; c < n; c += 256) {
+        const int ic = c < K ? c : -1;
+        const double cc = c < K ? tot_all[c] : *tot_x;
+        int rank = 0;
+        for (int c2 = 0; c2 < n; ++c2) {
+            const int ic2 = c2 < K ? c2 : -1;
+            const double x = c2 < K ? tot_all[c2] : *tot_x;
+            if (x < cc || (x == cc && ic2 < ic)) ++rank;
+        }
+        if (rank < Kr) sel[rank] = ic;   // -1: the extra rollout
+    }
+}
+
+__global__ __launch_bounds__(256) void k_reuse_pack(int Kr, int J, int N, int first, int K_loc, const int* sel,
+                                                    const double* params, const double* state, double* slot,
+                                                    const int* stop)
+{
+    if (stop && *stop) return;
+    const size_t JN = (size_t)J * N, W = JN + N;
+    for (size_t idx = blockIdx.x * 256 + threadIdx.x; idx < (size_t)Kr * W; idx += (size_t)gridDim.x * 256) {
+        const int r = (int)(idx / W);
+        const size_t off = idx % W;
+        const int src = sel[r] - first;
+        if (sel[r] < 0 || src < 0 || src >= K_loc) continue;   // another rank's row, or the extra
+        slot[idx] = off < JN ? params[(size_t)src * JN + off] : state[(size_t)src * N + (off - JN)];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_reuse_unpack(int Kr, int K_gen, int J, int N, int first, int K_loc,
+                                                      const int* sel, const double* slot_all, const double* x_params,
+                                                      const double* x_state, const double* theta, double* params,
+                                                      double* noise, double* state, const int* stop)
+{
+    if (stop && *stop) return;
+    const size_t JN = (size_t)J * N, W = JN + N;
+    for (size_t idx = blockIdx.x * 256 + threadIdx.x; idx < (size_t)Kr * W; idx += (size_t)gridDim.x * 256) {
+        const int r = (int)(idx / W);
+        const size_t off = idx % W;
+        const int dst = K_gen + r - first;
+        if (dst < 0 || dst >= K_loc) continue;
+        const int src = sel[r];
+        double v;
+        if (src < 0) v = off < JN ? x_params[off] : x_state[off - JN];
+        else v = slot_all[((size_t)(src / K_loc) * Kr + r) * W + off];
+        if (off < JN) {
+            params[(size_t)dst * JN + off] = v;
+            noise[(size_t)dst * JN + off] = v - theta[off];
+        } else {
+            state[(size_t)dst * N + (off - JN)] = v;
+        }
+    }
+}
+
+void launch_reuse_totals(int K_loc, int J, int N, const double* state, const double* control, const double* x_state,
+                         const double* x_control, double* tot_loc, double* tot_x, const int* stop, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_reuse_totals, dim3((K_loc + 1 + 255) / 256), dim3(256), 0, s, K_loc, J, N, state, control,
+                       x_state, x_control, tot_loc, tot_x, stop);
+}
+
+void launch_reuse_select(int K, int Kr, int with_extra, const double* tot_all, const double* tot_x, int* sel,
+                         const int* stop, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_reuse_select, dim3(1), dim3(256), 0, s, K, Kr, with_extra, tot_all, tot_x, sel, stop);
+}
+
+void launch_reuse_pack(int Kr, int J, int N, int first, int K_loc, const int* sel, const double* params,
+                       const double* state, double* slot, const int* stop, hipStream_t s)
+{
+    const size_t n = (size_t)Kr * ((size_t)J * N + N);
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_reuse_pack, dim3(blocks), dim3(256), 0, s, Kr, J, N, first, K_loc, sel, params, state, slot,
+                       stop);
+}
+
+void launch_reuse_unpack(int Kr, int K_gen, int J, int N, int first, int K_loc, const int* sel,
+                         const double* slot_all, const double* x_params, const double* x_state, const double* theta,
+                         double* params, double* noise, double* state, const int* stop, hipStream_t s)
+{
+    const size_t n = (size_t)Kr * ((size_t)J * N + N);
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_reuse_unpack, dim3(blocks), dim3(256), 0, s, Kr, K_gen, J, N, first, K_loc, sel, slot_all,
+                       x_params, x_state, theta, params, noise, state, stop);
 }
 
 // StompOptimizer::optimize bookkeeping (stomp_optimizer.cpp:301-344) for iteration index `it`

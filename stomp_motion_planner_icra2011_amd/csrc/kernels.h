@@ -305,6 +305,16 @@ void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double
                   double* state, const double* control, const double* x_params, const double* x_state,
                   const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
                   const int* stop, hipStream_t s);
+// sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
+void launch_reuse_totals(int K_loc, int J, int N, const double* state, const double* control, const double* x_state,
+                         const double* x_control, double* tot_loc, double* tot_x, const int* stop, hipStream_t s);
+void launch_reuse_select(int K, int Kr, int with_extra, const double* tot_all, const double* tot_x, int* sel,
+                         const int* stop, hipStream_t s);
+void launch_reuse_pack(int Kr, int J, int N, int first, int K_loc, const int* sel, const double* params,
+                       const double* state, double* slot, const int* stop, hipStream_t s);
+void launch_reuse_unpack(int Kr, int K_gen, int J, int N, int first, int K_loc, const int* sel,
+                         const double* slot_all, const double* x_params, const double* x_state, const double* theta,
+                         double* params, double* noise, double* state, const int* stop, hipStream_t s);
 void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes /*n x 6 idx ranges*/,
                       int nb, const long long* cyl_d2 /*nc x nx x ny*/, const int* cyl_z /*nc x 2*/, int nc,
                       float* out, hipStream_t s);

@@ -35,9 +35,12 @@ def on_threads(engines, fn):
         return [f.result(timeout=300) for f in futs]
 
 
-@pytest.mark.parametrize("world,K", [(2, 256), (4, 256)])
-def test_ranks_iterate_bitwise(world, K):
-    p = pb.make_problem(grid_n=64, num_rollouts=K, num_reused_rollouts=0)
+@pytest.mark.parametrize("world,K,Kr", [(2, 256, 0), (4, 256, 0), (2, 128, 64), (4, 256, 90), (8, 512, 200)])
+def test_ranks_iterate_bitwise(world, K, Kr):
+    """Kr > 0: the reuse ranking over all ranks' rows (all-gathered totals), the chosen rows moved
+    to their destination shard (policy_improvement.cpp:176-225); 90 and 200 reused rows straddle
+    shard boundaries"""
+    p = pb.make_problem(grid_n=64, num_rollouts=K, num_reused_rollouts=Kr)
     engines = make_ranks(p, world)
     K_loc = K // world
     for r, e in enumerate(engines):
@@ -99,10 +102,12 @@ def test_eight_ranks_cfg2_strong_scaling_shape():
         e.close()
 
 
-def test_ranks_optimize_loop():
-    # the device-resident optimize loop on every rank (identical stop decisions)
-    p = pb.make_problem(grid_n=64, num_rollouts=128, num_reused_rollouts=0, max_iterations=30,
-                        max_iterations_after_collision_free=1000)
+@pytest.mark.parametrize("Kr,after_cf", [(0, 1000), (64, 1000), (40, 3)])
+def test_ranks_optimize_loop(Kr, after_cf):
+    # the device-resident optimize loop on every rank (identical stop decisions), with and
+    # without reuse across the shards
+    p = pb.make_problem(grid_n=64, num_rollouts=128, num_reused_rollouts=Kr, max_iterations=30,
+                        max_iterations_after_collision_free=after_cf)
     engines = make_ranks(p, 2)
     o = po.Oracle(p, threads=THREADS)
     ost, ocosts = o.optimize()
