@@ -192,8 +192,8 @@ class Oracle:
         self._joints = _arr([so_joint(int(j.has_limits), j.min, j.max, j.joint_cost) for j in p.robot.joints], so_joint)
         self._sdf = np.ascontiguousarray(p.sdf, dtype=np.float32)
         pr = p.params
-        self._sig = np.full(self.J, pr.noise_stddev, np.float64)
-        self._dec = np.full(self.J, pr.noise_decay, np.float64)
+        self._sig = pr.per_joint("noise_stddev", self.J)
+        self._dec = pr.per_joint("noise_decay", self.J)
         self._start = np.ascontiguousarray(p.start, np.float64)
         self._goal = np.ascontiguousarray(p.goal, np.float64)
         g = p.grid

@@ -1191,8 +1191,11 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "padding FK failed: %s", hipGetErrorString(hipGetLastError())));
     m.pad_collision = pad_cf;
     e->pad_collision = pad_cf;
-    hipMemcpyAsync(e->d_last_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
-    hipMemcpyAsync(e->d_best_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream);
+    if (hipMemcpyAsync(e->d_last_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(e->d_best_traj, e->d_theta, sizeof(double) * J * N, hipMemcpyDeviceToDevice, e->stream) !=
+            hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "trajectory copies failed"));
 
     const bool local_id = world > 1 && std::memcmp(d->comm_id, kLocalMagic, sizeof kLocalMagic) == 0;
     if (local_id) {
@@ -1783,9 +1786,16 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
     if (!br.empty() && hipMalloc(&d_b, br.size() * sizeof(int)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
     if (!cd2.empty() && hipMalloc(&d_c, cd2.size() * sizeof(long long)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
     if (!cz.empty() && hipMalloc(&d_z, cz.size() * sizeof(int)) != hipSuccess) return fail(nullptr, STOMP_E_DEVICE, "hipMalloc");
-    if (d_b) hipMemcpyAsync(d_b, br.data(), br.size() * sizeof(int), hipMemcpyHostToDevice, s);
-    if (d_c) hipMemcpyAsync(d_c, cd2.data(), cd2.size() * sizeof(long long), hipMemcpyHostToDevice, s);
-    if (d_z) hipMemcpyAsync(d_z, cz.data(), cz.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    hipError_t cp = hipSuccess;
+    if (d_b) cp = hipMemcpyAsync(d_b, br.data(), br.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    if (d_c && cp == hipSuccess) cp = hipMemcpyAsync(d_c, cd2.data(), cd2.size() * sizeof(long long), hipMemcpyHostToDevice, s);
+    if (d_z && cp == hipSuccess) cp = hipMemcpyAsync(d_z, cz.data(), cz.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    if (cp != hipSuccess) {
+        if (d_b) hipFree(d_b);
+        if (d_c) hipFree(d_c);
+        if (d_z) hipFree(d_z);
+        return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(cp));
+    }
     launch_sdf_build(nx, ny, nz, cap2, res, d_b, (int)br.size() / 6, d_c, d_z, (int)cz.size() / 2, out, s);
     hipError_t st = hipStreamSynchronize(s);
     if (d_b) hipFree(d_b);

@@ -375,8 +375,18 @@ class StompParameters:
     use_cumulative_costs: bool = False
     num_rollouts: int = 10
     num_reused_rollouts: int = 5
-    noise_stddev: float = 2.0
-    noise_decay: float = 0.999
+    noise_stddev: object = 2.0     # one value for every joint, or a per-joint list (params.yaml:19-26)
+    noise_decay: object = 0.999
+
+    def per_joint(self, name: str, J: int) -> np.ndarray:
+        """noise_stddev / noise_decay as the J-vector PolicyImprovementLoop reads
+        (policy_improvement_loop.cpp:99-100); a list must have one entry per joint."""
+        v = np.asarray(getattr(self, name), np.float64)
+        if v.ndim == 0:
+            return np.full(J, float(v))
+        if v.shape != (J,):
+            raise ValueError(f"{name} has {v.size} entries for {J} joints")
+        return v.copy()
 
     @property
     def num_time_steps(self) -> int:

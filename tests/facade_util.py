@@ -20,8 +20,8 @@ def write_problem(p, directory):
         rows.append(" ".join(map(repr, [int(j.has_limits), float(j.min), float(j.max), float(j.joint_cost)])))
     rows.append(" ".join(map(repr, map(float, p.start))))
     rows.append(" ".join(map(repr, map(float, p.goal))))
-    rows.append(" ".join([repr(float(pr.noise_stddev))] * p.J))
-    rows.append(" ".join([repr(float(pr.noise_decay))] * p.J))
+    rows.append(" ".join(map(repr, map(float, pr.per_joint("noise_stddev", p.J)))))
+    rows.append(" ".join(map(repr, map(float, pr.per_joint("noise_decay", p.J)))))
     rows.append(" ".join(map(repr, [float(pr.trajectory_discretization), int(pr.max_iterations),
                                     int(pr.max_iterations_after_collision_free), float(pr.smoothness_cost_weight),
                                     float(pr.obstacle_cost_weight), float(pr.smoothness_cost_velocity),

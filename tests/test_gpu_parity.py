@@ -101,6 +101,16 @@ def test_iterations_bitwise(K, Kr):
         _compare_iteration(o, e, it)
 
 
+def test_per_joint_noise_schedule_bitwise():
+    # params.yaml:19-26 gives noise_stddev / noise_decay per joint (policy_improvement_loop.cpp:155-160)
+    sig = [2.0, 1.5, 3.0, 0.5, 2.5, 1.0, 4.0]
+    dec = [0.999, 0.995, 1.0, 0.99, 0.999, 0.98, 0.995]
+    p = make(K=20, Kr=10, noise_stddev=sig, noise_decay=dec)
+    o, e = po.Oracle(p), eng.Engine(p)
+    for it in range(1, 6):
+        _compare_iteration(o, e, it)
+
+
 def test_cumulative_costs_bitwise():
     p = make(K=16, use_cumulative_costs=True)
     o, e = po.Oracle(p), eng.Engine(p)
