@@ -127,7 +127,27 @@ __device__ __forceinline__ double round_nonneg(double u)
     return t + ((u - t) >= 0.5 ? 1.0 : 0.0);
 }
 
-#ifndef SDF_LEGACY_ROUND
+#if !defined(SDF_LEGACY_ROUND) && !defined(SDF_TRUNC_ROUND)
+// The same cell rule with fewer operations.  With u = (p - o) * (1/res):
+//   round(u) >= 1      <=>  u >= 0.5
+//   round(u) <= n - 2  <=>  u < n - 1.5        (n - 1.5 is exact)
+// and for u >= 0.5, floor(u + 0.5) == round(u): u + 0.5 is exact below 2^52 except when it
+// crosses into the next binade, and there it rounds onto the same integer round(u) gives (the
+// one value where floor(u + 0.5) != round(u) for u >= 0, u = 0.5 - 2^-54, is below 0.5 and
+// rejected by the range test).  So the range test moves onto u and each axis costs sub, mul,
+// two compares, add and floor.
+__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
+{
+    const double ux = (p[0] - m.ox) * m.inv_res;
+    const double uy = (p[1] - m.oy) * m.inv_res;
+    const double uz = (p[2] - m.oz) * m.inv_res;
+    const bool ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
+    const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
+    const unsigned idx = (unsigned)(ok ? cell : 0.0);
+    const float v = m.sdf[idx];
+    return ok ? v : 0.0f;
+}
+#elif defined(SDF_TRUNC_ROUND)
 __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
 {
     const double fx = round_nonneg((p[0] - m.ox) * m.inv_res);

@@ -141,6 +141,11 @@ struct stomp_engine {
     int pre_host = 1;
     int pre_it = -1;                  // iteration whose rows are in d_pre_eps / d_pre_meps[it & 1] (enqueued)
     double *d_pre_eps[2] = {nullptr, nullptr}, *d_pre_meps[2] = {nullptr, nullptr};
+    // the last iteration left its rows in d_pre_eps (rows_eps) instead of copying them into
+    // d_noise / d_params (run / iterate with pregen rows); materialize_rows writes them on demand
+    bool rows_in_pre = false;
+    const double* rows_eps = nullptr;
+    double* d_theta_gen = nullptr;
     double* h_total = nullptr;
     uint8_t* h_cf = nullptr;
     // eval scratch
@@ -495,6 +500,14 @@ void launch_noiseless(stomp_engine* e, int member)
     track_noiseless(e, ca);
 }
 
+// noise / params rows of an iteration that left them in its pregen buffer
+void materialize_rows(stomp_engine* e)
+{
+    if (!e->rows_in_pre) return;
+    launch_materialize_rows(e->K_loc, e->J * e->N, e->rows_eps, e->d_theta_gen, e->d_noise, e->d_params, e->stream);
+    e->rows_in_pre = false;
+}
+
 int flush_noiseless(stomp_engine* e)
 {
     if (e->pending_member >= 0) {
@@ -588,6 +601,7 @@ NoiseArgs noise_args(const stomp_engine* e, int it)
     na.params = e->d_params; na.noise = e->d_noise; na.control = e->d_control; na.zero_noise = 0; na.row_begin = 0;
     na.stop = e->d_stop;
     na.pre_eps = e->d_pre_eps[it & 1]; na.pre_meps = e->d_pre_meps[it & 1];
+    na.rows_in_pre = 0; na.theta_gen = e->d_theta_gen;
     return na;
 }
 
@@ -663,6 +677,13 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     if (fused) na.row_begin = num_gen;
     // every local row generated (K_r = 0): eps and M eps come from k_pregen
     const bool pre = fused && e->pre_on && num_gen == e->K_loc;
+    // outside the optimize loop the rows stay in the pregen buffer: the weights read eps there
+    // and nothing else needs the noise / params rows on the device (reuse is off with pregen).
+    // The optimize loop keeps the copies: after its stop the pregen blocks of the iterations
+    // enqueued past it still overwrite the buffers.
+    const bool rows_pre = pre && !e->tracking;
+    na.rows_in_pre = rows_pre ? 1 : 0;
+    if (!rows_pre) e->rows_in_pre = false;
     if (pre) {
         if (e->pre_it != it) {   // not made ahead by the previous iteration's launches
             Timed tm(e, T_PREGEN);
@@ -697,6 +718,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             Timed tm(e, T_COST);
             launch_rollouts(e, ca);
         }
+        if (rows_pre) {
+            e->rows_in_pre = true;
+            e->rows_eps = na.pre_eps;
+        }
         launch_terms_for(e, ca);
         // before this iteration's weights / update: a break decided on the previous
         // iteration's noiseless rollout leaves theta where the reference leaves it
@@ -705,7 +730,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     WeightArgs wa{};
     wa.stop = e->d_stop;
     wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
-    wa.state = e->d_state; wa.control = e->d_control; wa.noise = e->d_noise;
+    wa.state = e->d_state; wa.control = e->d_control; wa.noise = rows_pre ? na.pre_eps : e->d_noise;
     wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
     wa.tc = weights_tile(e->K_loc);
     wa.nb_total = e->K / kSumBlock;
@@ -976,6 +1001,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             CREATE_TRY(dev_alloc(e, &e->d_pre_eps[b], KJN));
             CREATE_TRY(dev_alloc(e, &e->d_pre_meps[b], KJN));
         }
+    if (e->pre_on) CREATE_TRY(dev_alloc(e, &e->d_theta_gen, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_params, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_noise, (size_t)J * N));
     CREATE_TRY(dev_alloc(e, &e->d_x_control, (size_t)J * N));
@@ -1158,6 +1184,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     e->tq_model.segs = m.segs;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
     m.ny_d = (double)m.ny; m.nz_d = (double)m.nz;
+    m.hi_x = m.nx - 1.5; m.hi_y = m.ny - 1.5; m.hi_z = m.nz - 1.5;
     m.ox = d->grid.origin[0]; m.oy = d->grid.origin[1]; m.oz = d->grid.origin[2]; m.res = d->grid.resolution;
     m.inv_res = 1.0 / d->grid.resolution;
     m.start = e->d_start; m.goal = e->d_goal;
@@ -1378,6 +1405,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
 {
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
+    materialize_rows(e);
     flush_noiseless(e);
     DevTrack init{};
     init.stop = 0; init.cfi = 0; init.iterations = 0; init.success = 0;
@@ -1482,6 +1510,7 @@ int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* nois
 {
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
+    materialize_rows(e);
     if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
     if (!noise_stddev) return fail(e, STOMP_E_INVALID, "null noise_stddev");
     flush_noiseless(e);
@@ -1509,6 +1538,7 @@ int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double cont
 {
     if (!e || !costs) return fail(e, STOMP_E_INVALID, "null argument");
     DeviceGuard dg(e->device);
+    materialize_rows(e);
     const int K = e->K, J = e->J, N = e->N;
     // state costs of the generated rows; reused rows keep theirs (policy_improvement.cpp:270-273)
     HIP_TRY(e, hipMemcpyAsync(e->d_state, costs, sizeof(double) * e->K_gen * N, hipMemcpyHostToDevice, e->stream));
@@ -1549,6 +1579,7 @@ int stomp_pi_improve_policy(stomp_engine* e, double* updates)
 {
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
+    materialize_rows(e);
     if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
     WeightArgs wa{};
     wa.stop = nullptr;
@@ -1578,6 +1609,7 @@ int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* para
 {
     if (!e || !params || !costs) return fail(e, STOMP_E_INVALID, "null argument");
     DeviceGuard dg(e->device);
+    materialize_rows(e);
     if (num != 1) return fail(e, STOMP_E_INVALID, "one extra rollout (the loop's noiseless rollout)");
     const int J = e->J, N = e->N;
     const size_t JN = (size_t)J * N;
@@ -1630,6 +1662,7 @@ int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
     const size_t KJN = (size_t)e->K_loc * e->J * e->N;
     const double* src = nullptr;
     size_t n = KJN;
+    if (!std::strcmp(which, "params") || !std::strcmp(which, "noise")) materialize_rows(e);
     if (!std::strcmp(which, "params")) src = e->d_params;
     else if (!std::strcmp(which, "noise")) src = e->d_noise;
     else if (!std::strcmp(which, "control_costs")) src = e->d_control;

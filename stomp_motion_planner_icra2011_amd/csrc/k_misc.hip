@@ -277,6 +277,24 @@ void launch_reuse_unpack(int Kr, int K_gen, int J, int N, int first, int K_loc, 
                        x_params, x_state, theta, params, noise, state, stop);
 }
 
+__global__ __launch_bounds__(256) void k_materialize_rows(size_t n, int JN, const double* eps, const double* theta_gen,
+                                                          double* noise, double* params)
+{
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const double e = eps[i];
+        noise[i] = e;
+        params[i] = theta_gen[i % JN] + e;   // the rollout kernel's theta + eps
+    }
+}
+
+void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,
+                             double* params, hipStream_t s)
+{
+    const size_t n = (size_t)K_loc * JN;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_materialize_rows, dim3(blocks), dim3(256), 0, s, n, JN, eps, theta_gen, noise, params);
+}
+
 // StompOptimizer::optimize bookkeeping (stomp_optimizer.cpp:301-344) for iteration index `it`
 // (iteration_), after its noiseless rollout: collision-free streak, success / collision-success
 // iterations, the cost history, best_group_trajectory_ (copied by the whole block) and the

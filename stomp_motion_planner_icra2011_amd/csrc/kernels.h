@@ -72,6 +72,7 @@ struct DevModel {
     int nx, ny, nz;
     double ox, oy, oz, res, inv_res;
     double ny_d, nz_d;          // ny, nz as doubles (the fp64 cell index of sdf_distance)
+    double hi_x, hi_y, hi_z;    // n - 1.5 per axis: round(u) <= n - 2 <=> u < n - 1.5
     const double* start;        // [J]
     const double* goal;         // [J]
     double vel_coef[7];         // invTime * DIFF_RULES[0][k]
@@ -145,6 +146,9 @@ struct NoiseArgs {
     int row_begin;              // only rows [row_begin, K_loc) (reused rows after the reuse kernel)
     double* pre_eps;            // [K_loc][J][N] eps = sigma L z made ahead of the rollout launch (k_pregen)
     double* pre_meps;           // [K_loc][J][N] M eps, likewise
+    int rows_in_pre;            // pregen rows: leave eps in pre_eps (no noise / params row copies;
+                                // the weights read pre_eps, stomp_engine_get_rollouts rebuilds them)
+    double* theta_gen;          // with rows_in_pre: rollout 0 keeps the theta the rows were made from
 };
 
 // Task::execute batch: blocks [0, num_noisy) evaluate params rows; block num_noisy (if
@@ -306,6 +310,9 @@ void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double
                   const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
                   const int* stop, hipStream_t s);
 // sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
+// noise = eps, params = theta_gen + eps of rows left in a pregen buffer (rows_in_pre)
+void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,
+                             double* params, hipStream_t s);
 void launch_reuse_totals(int K_loc, int J, int N, const double* state, const double* control, const double* x_state,
                          const double* x_control, double* tot_loc, double* tot_x, const int* stop, hipStream_t s);
 void launch_reuse_select(int K, int Kr, int with_extra, const double* tot_all, const double* tot_x, int* sel,

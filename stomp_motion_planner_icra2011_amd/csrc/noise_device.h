@@ -500,8 +500,12 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
                 const int d = idx / N, i = idx - d * N;
                 const double p = th[u] + e[u];
                 traj[idx] = p;
-                a.noise[row + idx] = e[u];
-                a.params[row + idx] = p;
+                if (!a.rows_in_pre) {
+                    a.noise[row + idx] = e[u];
+                    a.params[row + idx] = p;
+                } else if (r == 0) {
+                    a.theta_gen[idx] = th[u];
+                }
                 xs[d * Nall + i + 6] = p + mp[u];
             }
         }
