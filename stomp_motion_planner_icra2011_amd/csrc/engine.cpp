@@ -1133,6 +1133,18 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
                             m.sph_chunk, N));
         m.nsaves = 0;
         for (const FkOp& o : e->ops) m.nsaves = std::max(m.nsaves, o.save + 1);
+        // the sincos pre-pass parks the cosines in the saved-frame area: only when that area
+        // holds J x N doubles and the first save comes after the last joint segment
+        int last_joint = -1, first_save = (int)e->ops.size();
+        for (int i = 0; i < (int)e->ops.size(); ++i) {
+            const FkOp& o = e->ops[i];
+            if (o.seg >= 0 && segs[o.seg].q_index >= 0) last_joint = i;
+            if (o.save >= 0 && first_save == (int)e->ops.size()) first_save = i;
+        }
+        m.sincos_pre = m.nsaves >= 1 && J <= 12 * m.nsaves && first_save > last_joint ? 1 : 0;
+#ifdef NO_SINCOS_PRE
+        m.sincos_pre = 0;
+#endif
         // padding-row positions go to LDS unless that costs a workgroup per CU the launch
         // would use: one rollout launch has K_loc + 1 workgroups over the device's CUs
         const size_t stat = rollout_static_lds();

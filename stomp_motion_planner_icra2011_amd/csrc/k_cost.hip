@@ -280,7 +280,14 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         if (o.seg < 0 || !fk_lane) return;
         const DevSegment& sg = seg_s[o.seg];
         double st = 0.0, ct = 1.0;
-        if (sg.q_index >= 0) det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
+        if (sg.q_index >= 0) {
+            if (m.sincos_pre) {
+                st = traj[sg.q_index * N + t_own];
+                ct = sv[sg.q_index * N + t_own];
+            } else {
+                det_sincos(traj[sg.q_index * N + t_own], &st, &ct);
+            }
+        }
         Frame nf;
         if (o.base == kBaseChain) {
             compose(sg, &C, st, ct, nf);
@@ -314,6 +321,28 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
         return m.nops;
     };
+    if (m.sincos_pre) {
+        // every joint angle's (sin, cos) by all lanes, three independent chains per lane, so the
+        // FK lanes' chain is frame products only
+        // (each element is read and overwritten by one lane; a clamped read past the end may see a
+        // sine already stored there, and its result is discarded)
+        const int JN = J * N;
+        for (int i0 = tid; i0 - tid < JN; i0 += 3 * BLOCK) {
+            double q[3], sn[3], cs[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) q[u] = traj[min(i0 + u * BLOCK, JN - 1)];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) det_sincos(q[u], &sn[u], &cs[u]);
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                if (i0 + u * BLOCK < JN) {
+                    traj[i0 + u * BLOCK] = sn[u];
+                    sv[i0 + u * BLOCK] = cs[u];
+                }
+            }
+        }
+        __syncthreads();
+    }
     int op = fk_advance(0);
     int run = 0;   // sphere runs done (stamp index only)
     STAMP(7);

@@ -61,6 +61,9 @@ struct DevModel {
     int J, N, Nall, S, nops, nseg, nslots, sph_chunk;   // sph_chunk: most spheres on one segment
     int nsaves;                 // saved branch-point frames the FK program uses (0..kSaves, LDS)
     int pad_lds;                // padding-row positions staged in LDS (1) or read from HBM (0)
+    int sincos_pre;             // every (sin, cos) of the joint-limited trajectory made before the FK
+                                // program by all lanes: sines over traj, cosines in the saved-frame
+                                // area (the program's first save comes after its last joint segment)
     const unsigned long long* img;   // the rollout kernel's LDS table image (RolloutLds from .sph on)
     int img_words;              // 8-byte words of it copied to LDS (up to .pad, or .total with pad_lds)
     const DevSegment* segs;
