@@ -113,3 +113,100 @@ def test_two_rank_reduction_is_bitwise_single_rank():
     for rank, P, theta in res:
         np.testing.assert_array_equal(P, ref["prob"][rank * K_loc:(rank + 1) * K_loc])
         np.testing.assert_array_equal(theta, ref["theta1"])
+
+
+# ---- rollout reuse across ranks (K_r > 0; engine.cpp begin_generate, k_misc.hip k_reuse_*):
+# every rank prices its own rows (Rollout::getCost, policy_improvement.cpp:149-156), the totals
+# are all-gathered, every rank ranks all K + 1 candidates the way std::sort orders the
+# (cost, index) pairs (the extra rollout at index -1, :176-205), the owners pack the chosen rows
+# into slot r, the slots are all-gathered and every rank unpacks the reused rows it owns (rows
+# K_gen + r, noise re-based on the current theta, :209-223).
+KR_K, KR_KR = 128, 70     # K_gen = 58: the reused rows straddle the two shards
+
+
+def _reuse_reference():
+    p = pb.make_problem(grid_n=32, num_rollouts=KR_K, num_reused_rollouts=KR_KR)
+    o = po.Oracle(p, threads=1)
+    o.iterate(1)
+    before = dict(params=o.rollouts("params"), state=o.rollouts("state_costs"), control=o.rollouts("control_costs"),
+                  x_params=o.rollouts("x_params"), x_state=o.rollouts("x_state_costs"),
+                  x_control=o.rollouts("x_control_costs"), theta=o.theta())
+    o.iterate(2)
+    after = dict(params=o.rollouts("params"), noise=o.rollouts("noise"), state=o.rollouts("state_costs"))
+    return before, after
+
+
+def _get_cost(state, control):
+    s = state[0]
+    for t in range(1, len(state)):
+        s += state[t]
+    for d in range(control.shape[0]):
+        x = control[d, 0]
+        for t in range(1, control.shape[1]):
+            x += control[d, t]
+        s += x
+    return float("inf") if s != s else s
+
+
+def _reuse_worker(rank, world, port, before, out_q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    K_loc = KR_K // world
+    r0 = rank * K_loc
+    K_gen = KR_K - KR_KR
+    J, N = before["theta"].shape
+    tot = torch.tensor([_get_cost(before["state"][r], before["control"][r]) for r in range(r0, r0 + K_loc)],
+                       dtype=torch.float64)
+    parts = [torch.zeros(K_loc, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(parts, tot)
+    totals = torch.cat(parts).tolist()
+    cand = [(c, i) for i, c in enumerate(totals)] + [(_get_cost(before["x_state"], before["x_control"]), -1)]
+    sel = [i for _, i in sorted(cand)[:KR_KR]]
+    W = J * N + N
+    slot = np.zeros((KR_KR, W))
+    for r, src in enumerate(sel):
+        if src >= 0 and r0 <= src < r0 + K_loc:
+            slot[r, :J * N] = before["params"][src].reshape(-1)
+            slot[r, J * N:] = before["state"][src]
+    gathered = [torch.zeros(KR_KR, W, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(gathered, torch.from_numpy(slot))
+    rows = {}
+    for r, src in enumerate(sel):
+        dst = K_gen + r
+        if not (r0 <= dst < r0 + K_loc):
+            continue
+        if src < 0:
+            prm, st = before["x_params"].reshape(-1), before["x_state"]
+        else:
+            v = gathered[src // K_loc][r].numpy()
+            prm, st = v[:J * N], v[J * N:]
+        prm = prm.reshape(J, N)
+        rows[dst] = (prm.copy(), prm - before["theta"], st.copy())
+    out_q.put((rank, rows))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_reuse_is_bitwise_single_rank():
+    before, after = _reuse_reference()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reuse_worker, args=(r, 2, port, before, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen = set()
+    for rank, rows in res:
+        assert rows, f"rank {rank} owns reused rows"
+        for dst, (prm, nz, st) in rows.items():
+            np.testing.assert_array_equal(prm, after["params"][dst])
+            np.testing.assert_array_equal(nz, after["noise"][dst])
+            np.testing.assert_array_equal(st, after["state"][dst])
+            seen.add(dst)
+    assert seen == set(range(KR_K - KR_KR, KR_K))
