@@ -204,6 +204,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     // wave butterfly (every lane ends with the same (max, first index)) and a pass needs
     // no block barrier.  LDS accesses of one wave execute in program order.
     if (__syncthreads_or(any)) {
+        __builtin_amdgcn_s_setprio(3);   // one wave per limited joint: a dependent chain (critical path)
         for (int j = wv; j < J; j += NW) {
             if (!hl_s[j]) continue;
             const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
                 __builtin_amdgcn_wave_barrier();
             }
         }
+        __builtin_amdgcn_s_setprio(2);
         __syncthreads();
     }
     STAMP(2);
@@ -343,7 +345,13 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         }
         __syncthreads();
     }
+    // the FK chain and the ordered fold run on two waves while the other waves wait at the
+    // next barrier: they are this workgroup's critical path, so they take issue priority (3)
+    // over the co-resident workgroup's wide, VALU-heavy pair and velocity phases (2) and the
+    // pregen blocks (0)
+    __builtin_amdgcn_s_setprio(3);
     int op = fk_advance(0);
+    __builtin_amdgcn_s_setprio(2);
     int run = 0;   // sphere runs done (stamp index only)
     STAMP(7);
     while (op < m.nops) {
@@ -480,6 +488,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 #endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
+        __builtin_amdgcn_s_setprio(3);
         if (fk_lane) {
             // fold in sphere order; the LDS reads go out 16 at a time
             const int nsl = se - sb;
@@ -499,6 +508,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         // program's control flow is uniform, so every lane arrives at the same next op
         if (next < 0) next = fk_advance(op + 1);
         op = next;
+        __builtin_amdgcn_s_setprio(2);
         STAMP(13 + 4 * run);
         ++run;
     }
