@@ -471,7 +471,9 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 #endif
         __syncthreads();   // pots and the non-zero list complete
         STAMP(11 + 4 * run);
-        // velocities only for the listed pairs, spread densely over the block
+        // velocities only for the listed pairs, spread densely over the block: usually fewer
+        // pairs than lanes, one latency chain each, so at the critical-path priority too
+        __builtin_amdgcn_s_setprio(3);
         for (int i = tid; i < nz_count; i += BLOCK) {
             const int it = nzl[i];
             const int qi = it / N, ti = it - qi * N;
