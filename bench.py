@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--dof", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--problems", type=int, default=None, help="cfg5: problems of the whole job")
+    ap.add_argument("--enqueue-threads", type=int, default=1, help="cfg5: host threads enqueueing the problems")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event pass (no roofline)")
     ap.add_argument("--optimize-steps", type=int, default=200,
@@ -182,12 +183,27 @@ def bench_problems(args, world, rank, local_rank, dist):
                             max_iterations=args.warmup + args.steps + 1)
         engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr))
 
+    threads = max(1, min(args.enqueue_threads, len(engines)))
+    pool = None
+    if threads > 1:
+        import concurrent.futures as cf
+        pool = cf.ThreadPoolExecutor(threads)
+
     def sweep(first, count):
         # each problem's iterations as one stomp_engine_run (its noiseless rollouts ride in the
         # next rollout launch; a run of one iteration would flush each as its own launch); the
-        # problems' streams overlap on the device while the host enqueues the next problem
-        for e in engines:
-            e.run(first, count)
+        # problems' streams overlap on the device while the host enqueues the next problem.
+        # Enqueueing is the limit at several problems per GPU (three launches per problem-
+        # iteration), so host threads share it: distinct engines may be driven concurrently
+        # (stomp_engine.h), and the ctypes calls release the GIL
+        if pool is None:
+            for e in engines:
+                e.run(first, count)
+        else:
+            def part(k):
+                for e in engines[k::threads]:
+                    e.run(first, count)
+            list(pool.map(part, range(threads)))
         for e in engines:
             e.synchronize()
 
@@ -213,6 +229,7 @@ def bench_problems(args, world, rank, local_rank, dist):
                                    f"{args.grid}^3 SDF shared per GPU",
                        "problems": P_all, "parallelism": f"replicas x{world}, one stream per problem",
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                       "enqueue_threads": threads,
                        "rollouts_per_s": round(value * args.rollouts, 1)}}))
     for e in engines:
         e.close()
