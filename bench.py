@@ -7,7 +7,9 @@ Workloads (BASELINE.json configs; --workload, default cfg2 = configs[1], the met
   cfg3  7-DOF, 200 waypoints (N = 199), K = 4096, 256^3
   cfg4  14-DOF two-arm tree, 100 waypoints, K = 1024, 512^3 (the HBM-bound field)
   cfg5  64 independent problems (7-DOF, 100 wp, K = 128 each, distinct start / goal / seed),
-        one engine and stream per problem, 64 / N problems per GPU, no communication
+        64 / N problems per GPU, no communication; a GPU's problems form one engine group
+        (stomp_group_run: one rollout, weights and update launch per iteration for all of them;
+        --group 0 = one engine and stream per problem)
 A step is one PolicyImprovementLoop::runSingleIteration equivalent (noise, projection, control
 costs, K rollout executions, probability weighting, update, noiseless rollout), enqueued by
 stomp_engine_run with inputs already resident in HBM.  With --gpus N the K rollouts of the
@@ -63,6 +65,9 @@ def parse():
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--problems", type=int, default=None, help="cfg5: problems of the whole job")
     ap.add_argument("--enqueue-threads", type=int, default=1, help="cfg5: host threads enqueueing the problems")
+    ap.add_argument("--group", type=int, default=-1,
+                    help="cfg5: problems per engine group (shared launches; -1 = all of a GPU's problems, "
+                         "0 = one stream per problem)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event pass (no roofline)")
     ap.add_argument("--optimize-steps", type=int, default=200,
@@ -173,6 +178,8 @@ def bench_problems(args, world, rank, local_rank, dist):
                            num_reused_rollouts=0, build_grid=False)
     sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
     eng.sdf_build_device(base, sdf.ptr)
+    gsize = P if args.group < 0 else args.group
+    streams = [eng.Stream(local_rank) for _ in range((P + gsize - 1) // gsize)] if gsize else []
     engines = []
     offsets = rng.uniform(-0.15, 0.15, (P_all, 2, base.J))
     for i in range(first_id, first_id + P):
@@ -181,7 +188,12 @@ def bench_problems(args, world, rank, local_rank, dist):
                             num_rollouts=args.rollouts, num_reused_rollouts=0, build_grid=False,
                             seed=base.seed + 1 + i, start=list(base.start + d[0]), goal=list(base.goal + d[1]),
                             max_iterations=args.warmup + args.steps + 1)
-        engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr))
+        k = i - first_id
+        engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr,
+                                  stream=streams[k // gsize].ptr if gsize else None))
+    # --group G: the problems in groups of G engines on one stream each, every group advanced by
+    # shared launches (stomp_group_run: three dispatches per iteration for the whole group)
+    groups = [eng.EngineGroup(engines[k:k + gsize]) for k in range(0, P, gsize)] if gsize else []
 
     threads = max(1, min(args.enqueue_threads, len(engines)))
     pool = None
@@ -196,6 +208,12 @@ def bench_problems(args, world, rank, local_rank, dist):
         # Enqueueing is the limit at several problems per GPU (three launches per problem-
         # iteration), so host threads share it: distinct engines may be driven concurrently
         # (stomp_engine.h), and the ctypes calls release the GIL
+        if groups:
+            for g in groups:
+                g.run(first, count)
+            for g in groups:
+                g.synchronize()
+            return
         if pool is None:
             for e in engines:
                 e.run(first, count)
@@ -227,12 +245,16 @@ def bench_problems(args, world, rank, local_rank, dist):
             "config": {"workload": f"{workload_name(args)}: {P_all} problems over {world} GPU ({max(per)} per GPU), "
                                    f"{args.dof}-DOF, {args.waypoints} wp, K={args.rollouts} each, "
                                    f"{args.grid}^3 SDF shared per GPU",
-                       "problems": P_all, "parallelism": f"replicas x{world}, one stream per problem",
+                       "problems": P_all, "parallelism": f"replicas x{world}, " + (f"groups of {gsize} problems (shared launches)" if gsize else "one stream per problem"),
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                       "enqueue_threads": threads,
+                       "enqueue_threads": threads, "group": gsize,
                        "rollouts_per_s": round(value * args.rollouts, 1)}}))
+    for g in groups:
+        g.close()
     for e in engines:
         e.close()
+    for st in streams:
+        st.close()
     sdf.free()
 
 

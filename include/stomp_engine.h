@@ -303,6 +303,22 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
  * velocity, acceleration, jerk; 3 x 7 doubles, row-major).  Host only, no device needed. */
 int stomp_diff_rules(double* out);
 
+/* Groups: several engines of one shape (same J, N, K, spheres and model layout; single device,
+ * no reuse, no state-cost terms), created on ONE shared stream, advanced in lockstep by shared
+ * launches -- one rollout, one weights and one update launch per iteration for the whole group
+ * instead of three per engine (a batch of independent planning problems, BASELINE cfg5).  Each
+ * engine ends in exactly the state its own stomp_engine_run(first, count) leaves: its θ, rollouts
+ * and pending noiseless rollout; the engines' own calls keep working between group runs.
+ * stomp_group_synchronize flushes every engine's pending noiseless rollout and waits. */
+typedef struct stomp_group stomp_group;
+int stomp_stream_create(int32_t device, void** out_stream);
+int stomp_stream_destroy(void* stream);
+int stomp_group_create(stomp_engine* const* engines, int32_t num_engines, stomp_group** out);
+int stomp_group_run(stomp_group* g, int32_t first_iteration, int32_t count);
+int stomp_group_synchronize(stomp_group* g);
+const char* stomp_group_last_error(const stomp_group* g);
+void stomp_group_destroy(stomp_group* g);
+
 /* Device buffers for callers without a HIP runtime of their own (bench, tests). */
 int stomp_device_alloc(int32_t device, uint64_t bytes, void** out);
 int stomp_device_free(void* p);

@@ -2061,4 +2061,253 @@ int stomp_comm_unique_id(void* out128)
 #endif
 }
 
+
+// ===================================================================== engine groups
+// Several engines of one shape driven in lockstep by shared launches: per iteration one rollout
+// launch covering every engine's rollout workgroups and pregen blocks, one weights launch and one
+// update launch (k_rollout_group, k_weights_rows_group, k_update_group), so a batch of independent
+// planning problems costs three dispatches per iteration instead of three per problem.  The
+// per-engine kernel arguments of a whole run are staged in pinned memory and uploaded once; each
+// engine's results are the ones its own stomp_engine_run gives, bit for bit.
+
+int stomp_stream_create(int32_t device, void** out)
+{
+    if (!out) return fail(nullptr, STOMP_E_INVALID, "null argument");
+    DeviceGuard dg(device);
+    hipStream_t s = nullptr;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+        return fail(nullptr, STOMP_E_DEVICE, "hipStreamCreate failed");
+    *out = (void*)s;
+    return 0;
+}
+
+int stomp_stream_destroy(void* stream)
+{
+    if (stream && hipStreamDestroy((hipStream_t)stream) != hipSuccess)
+        return fail(nullptr, STOMP_E_DEVICE, "hipStreamDestroy failed");
+    return 0;
+}
+
+struct stomp_group {
+    std::vector<stomp_engine*> e;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int nt = 0;                           // weights tiles per engine
+    DevModel* d_models = nullptr;         // [P]
+    unsigned char* d_args = nullptr;      // [iterations][P] CostArgs, then WeightArgs, then UpdateArgs
+    size_t d_cap = 0;
+    unsigned char* h_args = nullptr;      // pinned staging of one run's arguments
+    size_t h_cap = 0;
+    hipEvent_t staged = nullptr;          // the last upload from h_args is done
+    std::string err;
+};
+
+namespace {
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int gfail(stomp_group* g, int code, const char* msg)
+{
+    g_last_error = msg;
+    if (g) g->err = msg;
+    return code;
+}
+}  // namespace
+
+void stomp_group_destroy(stomp_group* g)
+{
+    if (!g) return;
+    DeviceGuard dg(g->device);
+    if (g->staged) {
+        hipEventSynchronize(g->staged);
+        hipEventDestroy(g->staged);
+    }
+    if (g->d_models) hipFree(g->d_models);
+    if (g->d_args) hipFree(g->d_args);
+    if (g->h_args) hipHostFree(g->h_args);
+    delete g;
+}
+
+int stomp_group_create(stomp_engine* const* engines, int32_t n, stomp_group** out)
+{
+    if (!engines || n <= 0 || !out) return gfail(nullptr, STOMP_E_INVALID, "invalid group arguments");
+    stomp_engine* e0 = engines[0];
+    if (!e0) return gfail(nullptr, STOMP_E_INVALID, "null engine");
+    const size_t lds0 = rollout_lds_bytes(e0->model, e0->model.pad_lds);
+    for (int p = 0; p < n; ++p) {
+        stomp_engine* e = engines[p];
+        if (!e) return gfail(nullptr, STOMP_E_INVALID, "null engine");
+        if (e->device != e0->device || e->stream != e0->stream)
+            return gfail(nullptr, STOMP_E_INVALID, "the engines of a group share one device and one stream");
+        if (e->J != e0->J || e->N != e0->N || e->K != e0->K || e->S != e0->S ||
+            rollout_lds_bytes(e->model, e->model.pad_lds) != lds0)
+            return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model)");
+        if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->pre_host != 1 || e->terms_on || e->split ||
+            e->split_modes || e->use_cum || e->J > 16)
+            return gfail(nullptr, STOMP_E_UNSUPPORTED,
+                         "groups run single-device engines without reuse, state-cost terms or cumulative costs");
+    }
+    const int nt = weights_group_tiles(e0->J, e0->N, e0->K_loc);
+    if (nt <= 0) return gfail(nullptr, STOMP_E_UNSUPPORTED, "rollouts per engine beyond the weights tiles");
+    DeviceGuard dg(e0->device);
+    stomp_group* g = new stomp_group();
+    g->e.assign(engines, engines + n);
+    g->device = e0->device;
+    g->stream = e0->stream;
+    g->nt = nt;
+    std::vector<DevModel> ms(n);
+    for (int p = 0; p < n; ++p) ms[p] = engines[p]->model;
+    if (hipMalloc(&g->d_models, sizeof(DevModel) * n) != hipSuccess ||
+        hipMemcpy(g->d_models, ms.data(), sizeof(DevModel) * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess) {
+        stomp_group_destroy(g);
+        return gfail(nullptr, STOMP_E_DEVICE, "group allocation failed");
+    }
+    *out = g;
+    return 0;
+}
+
+const char* stomp_group_last_error(const stomp_group* g) { return g ? g->err.c_str() : g_last_error.c_str(); }
+
+int stomp_group_run(stomp_group* g, int32_t first, int32_t count)
+{
+    if (!g) return gfail(nullptr, STOMP_E_INVALID, "null group");
+    if (count <= 0) return 0;
+    DeviceGuard dg(g->device);
+    const int P = (int)g->e.size();
+    stomp_engine* e0 = g->e[0];
+    for (stomp_engine* e : g->e) {
+        // lockstep: the engines enter the run in one pipeline state
+        if (e->pending_member != e0->pending_member || e->pre_it != e0->pre_it || e->tracking)
+            return gfail(g, STOMP_E_INVALID, "the engines of a group are not at the same iteration state");
+    }
+    const size_t szc = align256(sizeof(CostArgs) * P), szw = align256(sizeof(WeightArgs) * P),
+                 szu = align256(sizeof(UpdateArgs) * P), per = szc + szw + szu;
+    const size_t bytes = per * (size_t)count;
+    if (g->staged && hipEventSynchronize(g->staged) != hipSuccess)   // h_args free again
+        return gfail(g, STOMP_E_DEVICE, "group staging wait failed");
+    if (bytes > g->h_cap) {
+        if (g->h_args) hipHostFree(g->h_args);
+        g->h_args = nullptr;
+        g->h_cap = 0;
+        if (hipHostMalloc((void**)&g->h_args, bytes) != hipSuccess) return gfail(g, STOMP_E_DEVICE, "hipHostMalloc failed");
+        g->h_cap = bytes;
+    }
+    if (bytes > g->d_cap) {
+        if (g->d_args) {
+            hipStreamSynchronize(g->stream);
+            hipFree(g->d_args);
+        }
+        g->d_args = nullptr;
+        g->d_cap = 0;
+        if (hipMalloc(&g->d_args, bytes) != hipSuccess) return gfail(g, STOMP_E_DEVICE, "hipMalloc failed");
+        g->d_cap = bytes;
+    }
+    std::vector<int> nro(count);
+    std::vector<char> pregen_first(P, 0);
+    for (int i = 0; i < count; ++i) {
+        const int it = first + i, member = it - 1;
+        CostArgs* cas = (CostArgs*)(g->h_args + per * i);
+        WeightArgs* was = (WeightArgs*)(g->h_args + per * i + szc);
+        UpdateArgs* uas = (UpdateArgs*)(g->h_args + per * i + szc + szw);
+        for (int p = 0; p < P; ++p) {
+            stomp_engine* e = g->e[p];
+            // enqueue_iteration's pipelined path with pregen rows, arguments only
+            int rc = begin_generate(e);   // K_r = 0: every row generated
+            if (rc) return rc;
+            NoiseArgs na = noise_args(e, it);
+            na.K_gen_global = e->K_gen;
+            na.row_begin = e->K_loc;
+            na.rows_in_pre = 1;
+            if (e->pre_it != it) {
+                if (i > 0) return gfail(g, STOMP_E_INVALID, "group pregen rows out of step");
+                pregen_first[p] = 1;
+            }
+            CostArgs ca{};
+            ca.stop = e->d_stop;
+            ca.fused_noise = 2;
+            ca.nz = na;
+            ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = e->K_loc;
+            ca.member = member; ca.state_out = e->d_state;
+            ca.pre_rows = e->K_loc;
+            ca.pre_next = pregen_args(e, it + 1);
+            e->pre_it = it + 1;
+            if (e->pending_member >= 0) {
+                ca.x_params = e->d_theta; ca.x_member = e->pending_member;
+                ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+                e->pending_member = -1;
+            }
+            const int n_ro = ca.num_noisy + (ca.x_params ? 1 : 0);
+            if (p == 0) nro[i] = n_ro;
+            else if (n_ro != nro[i]) return gfail(g, STOMP_E_INVALID, "group engines out of step");
+            e->rows_in_pre = true;
+            e->rows_eps = na.pre_eps;
+            cas[p] = ca;
+            WeightArgs wa{};
+            wa.stop = e->d_stop;
+            wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = 0;
+            wa.state = e->d_state; wa.control = e->d_control; wa.noise = na.pre_eps;
+            wa.prob = e->d_prob; wa.u = e->d_u;
+            wa.tc = weights_tile(e->K_loc);
+            wa.nb_total = e->K / kSumBlock;
+            wa.mode = W_FUSED;
+            was[p] = wa;
+            uas[p] = UpdateArgs{e->d_MT, e->d_u, e->d_theta, e->d_stop};
+            e->pending_member = member;
+        }
+    }
+    hipStream_t s = g->stream;
+    for (int p = 0; p < P; ++p)
+        if (pregen_first[p]) launch_pregen(pregen_args(g->e[p], first), g->e[p]->K_loc, s);
+    hipError_t err = hipMemcpyAsync(g->d_args, g->h_args, bytes, hipMemcpyHostToDevice, s);
+    if (err == hipSuccess) err = hipEventRecord(g->staged, s);
+    if (err != hipSuccess) return gfail(g, STOMP_E_DEVICE, "group argument upload failed");
+    const int J = e0->J, N = e0->N, K = e0->K_loc;
+    for (int i = 0; i < count; ++i) {
+        unsigned char* base = g->d_args + per * i;
+        launch_cost_group(e0->model, g->d_models, (const CostArgs*)base, P, nro[i], K, s);
+        launch_weights_group((const WeightArgs*)(base + szc), P, J, N, K, s);
+        launch_update_group(J, N, (const UpdateArgs*)(base + szc + szw), P, s);
+    }
+    err = hipGetLastError();
+    if (err != hipSuccess) return gfail(g, STOMP_E_DEVICE, hipGetErrorString(err));
+    return 0;
+}
+
+int stomp_group_synchronize(stomp_group* g)
+{
+    if (!g) return gfail(nullptr, STOMP_E_INVALID, "null group");
+    DeviceGuard dg(g->device);
+    const int P = (int)g->e.size();
+    bool all = true;
+    for (stomp_engine* e : g->e) all = all && e->pending_member >= 0 && !e->tracking;
+    if (all) {
+        // every engine's pending noiseless rollout in one launch (one workgroup per engine)
+        const size_t bytes = align256(sizeof(CostArgs) * P);
+        if (g->staged && hipEventSynchronize(g->staged) != hipSuccess)
+            return gfail(g, STOMP_E_DEVICE, "group staging wait failed");
+        if (bytes > g->h_cap || bytes > g->d_cap) {
+            all = false;   // the arrays of a run are larger; no run yet: per-engine flushes
+        } else {
+            CostArgs* cas = (CostArgs*)g->h_args;
+            for (int p = 0; p < P; ++p) {
+                stomp_engine* e = g->e[p];
+                CostArgs ca{};
+                ca.stop = e->d_stop;
+                ca.num_noisy = 0;
+                ca.x_params = e->d_theta; ca.x_member = e->pending_member;
+                ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+                cas[p] = ca;
+                e->pending_member = -1;
+            }
+            hipError_t err = hipMemcpyAsync(g->d_args, g->h_args, bytes, hipMemcpyHostToDevice, g->stream);
+            if (err == hipSuccess) err = hipEventRecord(g->staged, g->stream);
+            if (err != hipSuccess) return gfail(g, STOMP_E_DEVICE, "group argument upload failed");
+            launch_cost_group(g->e[0]->model, g->d_models, (const CostArgs*)g->d_args, P, 1, 0, g->stream);
+        }
+    }
+    for (stomp_engine* e : g->e) flush_noiseless(e);
+    if (hipStreamSynchronize(g->stream) != hipSuccess) return gfail(g, STOMP_E_DEVICE, "group synchronize failed");
+    return 0;
+}
+
 }  // extern "C"

@@ -99,8 +99,10 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x)
     return max(max(a, b), max(c, d));
 }
 
+// the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
+// k_rollout_group: the engines of a group share one launch)
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
+__device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ int flag;
@@ -113,11 +115,11 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
         // they take the issue slots the latency-bound rollout waves leave idle and the CUs
         // the early-finishing rollouts free; no stop check (the rows stay valid for pre_it)
         const int nro = a.num_noisy + (a.x_params ? 1 : 0);
-        if ((int)blockIdx.x >= nro) {
+        if (bid >= nro) {
             const NoiseArgs& pa = a.pre_next;
             double* pA = (double*)(lds_raw + L.nzA);
             double* pB = (double*)(lds_raw + L.nzB);
-            const int r = blockIdx.x - nro;
+            const int r = bid - nro;
             rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
             if (J <= 8) {
                 pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 
     STAMP(0);
     BLOCK_BEGIN();
-    const int e = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int e = bid, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int NW = BLOCK / 64;
     const bool extra = e == a.num_noisy;
     const int member = extra ? a.x_member : a.member;
@@ -548,6 +550,33 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
     BLOCK_END();
 }
 
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
+{
+    rollout_body<BLOCK>(m, a, blockIdx.x);
+}
+
+// one launch for the rollouts of a group of engines of one shape (stomp_group_run): every
+// engine's rollout workgroups first (engine p's nro of them at p nro), then every engine's
+// pregen blocks (npre each, at the default priority behind them all); models and arguments
+// live in device memory, one entry per engine
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout_group(const DevModel* ms, const CostArgs* as,
+                                                                           int engines, int nro, int npre)
+{
+    const int b = blockIdx.x;
+    int p, bid;
+    if (b < engines * nro) {
+        p = b / nro;
+        bid = b - p * nro;
+    } else {
+        const int j = b - engines * nro;
+        p = j / npre;
+        bid = nro + (j - p * npre);
+    }
+    rollout_body<BLOCK>(ms[p], as[p], bid);
+}
+
 STOMP_STAMP_ACCESSORS(cost)
 
 // generateRollouts' normals and eps = sigma L z, computeProjectedNoise's M eps for one row per
@@ -578,6 +607,16 @@ void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s)
     const RolloutLds L = rollout_lds(a.J, a.N, 0, 0, 0, 0, 0, 0, 0);
     const size_t lds = 2 * (L.nzB - L.nzA);
     hipLaunchKernelGGL((k_pregen<256>), dim3(rows), dim3(256), lds, s, a);
+}
+
+void launch_cost_group(const DevModel& m0, const DevModel* ms, const CostArgs* as, int engines, int nro, int npre,
+                       hipStream_t s)
+{
+    const int blocks = engines * (nro + npre);
+    if (blocks <= 0) return;
+    const size_t lds = rollout_lds_bytes(m0, m0.pad_lds);
+    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kBlock>, lds);
+    hipLaunchKernelGGL((k_rollout_group<kBlock>), dim3(blocks), dim3(kBlock), lds, s, ms, as, engines, nro, npre);
 }
 
 bool cost_supported(const DevModel& m)

@@ -408,6 +408,15 @@ __global__ __launch_bounds__(kWRB) void k_weights_rows(WeightArgs a)
     weights_rows<TCW, EPT>(a, blockIdx.x, gridDim.x, V);
 }
 
+// the weights tiles of a group of engines in one launch (engine p's nt tiles at p nt)
+template <int TCW, int EPT>
+__global__ __launch_bounds__(kWRB) void k_weights_rows_group(const WeightArgs* as, int nt)
+{
+    extern __shared__ __attribute__((aligned(16))) double V[];
+    const int p = blockIdx.x / nt;
+    weights_rows<TCW, EPT>(as[p], blockIdx.x - p * nt, nt, V);
+}
+
 // The same launch also carries k_pregen's rows for the next iteration (blocks nw on): the
 // weights tiles occupy under 256 workgroups, so the theta-independent noise of iteration
 // it + 1 (normals, sigma L z, M eps; noise_device.h) fills the idle CUs in the same dispatch
@@ -537,11 +546,12 @@ constexpr int kUpdateBatch = UPDATE_BATCH;
 #define UPDATE_XPRE false
 #endif
 
-__global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
-                                                int nb_total, double* theta, const int* stop, double* delta)
+__device__ __forceinline__ void update_body(int d, int J, int N, const double* MT, const double* u,
+                                            const double* u_all, int nb_total, double* theta, const int* stop,
+                                            double* delta)
 {
     __shared__ double us[256 + 2 * kUpdateBatch];
-    const int d = blockIdx.x, i = threadIdx.x;
+    const int i = threadIdx.x;
     // everything independent is issued up front: the stop flag (checked at the store), this
     // lane's u entry, then (inside band_tile) the first M rows; the LDS fill and its barrier
     // run while those rows are in flight
@@ -569,6 +579,56 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
     if (i >= N || stopped) return;
     if (delta) delta[(size_t)d * N + i] = s;   // improvePolicy's update alone (PolicyImprovement API)
     else theta[(size_t)d * N + i] += 1.0 * s;
+}
+
+__global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
+                                                int nb_total, double* theta, const int* stop, double* delta)
+{
+    update_body(blockIdx.x, J, N, MT, u, u_all, nb_total, theta, stop, delta);
+}
+
+// the updates of a group of engines in one launch (engine p's joint d at p J + d)
+__global__ __launch_bounds__(256) void k_update_group(int J, int N, const UpdateArgs* as)
+{
+    const int p = blockIdx.x / J;
+    const UpdateArgs& a = as[p];
+    update_body(blockIdx.x - p * J, J, N, a.MT, a.u, nullptr, 0, a.theta, a.stop, nullptr);
+}
+
+void launch_update_group(int J, int N, const UpdateArgs* as, int engines, hipStream_t s)
+{
+    if (engines > 0) hipLaunchKernelGGL(k_update_group, dim3(J * engines), dim3(256), 0, s, J, N, as);
+}
+
+// the rows path of launch_weights for a group (the engine checks rows_tiles() > 0)
+int weights_group_tiles(int J, int N, int K_loc)
+{
+    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
+    const int nb = (K_loc + kSumBlock - 1) / kSumBlock;
+    if (!(nb * WEIGHTS_ROWS_TCW <= kWRB) || K_loc > 32 * RS) return 0;
+    return (J * N + WEIGHTS_ROWS_TCW - 1) / WEIGHTS_ROWS_TCW;
+}
+
+void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K_loc, hipStream_t s)
+{
+    constexpr int TCW = WEIGHTS_ROWS_TCW, RS = kWRB / TCW;
+    const int nt = weights_group_tiles(J, N, K_loc);
+    if (nt <= 0 || engines <= 0) return;
+    const size_t lds = weights_rows_v_bytes(K_loc, TCW);
+    const dim3 grid(nt * engines);
+    if (K_loc <= 4 * RS) {
+        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 4>, lds);
+        hipLaunchKernelGGL((k_weights_rows_group<TCW, 4>), grid, dim3(kWRB), lds, s, as, nt);
+    } else if (K_loc <= 8 * RS) {
+        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 8>, lds);
+        hipLaunchKernelGGL((k_weights_rows_group<TCW, 8>), grid, dim3(kWRB), lds, s, as, nt);
+    } else if (K_loc <= 16 * RS) {
+        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 16>, lds);
+        hipLaunchKernelGGL((k_weights_rows_group<TCW, 16>), grid, dim3(kWRB), lds, s, as, nt);
+    } else {
+        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 32>, lds);
+        hipLaunchKernelGGL((k_weights_rows_group<TCW, 32>), grid, dim3(kWRB), lds, s, as, nt);
+    }
 }
 
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,

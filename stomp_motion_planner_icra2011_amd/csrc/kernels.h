@@ -305,6 +305,18 @@ int weights_tile(int K_loc);
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
                    double* theta, const int* stop, hipStream_t s, double* delta = nullptr);
 // out[i] = max over r < world of gathered[r][i] (the in-process group's all-reduce(max))
+// groups of engines of one shape in shared launches (stomp_group_run)
+struct UpdateArgs {
+    const double* MT;
+    const double* u;
+    double* theta;
+    const int* stop;
+};
+void launch_cost_group(const DevModel& m0, const DevModel* ms, const CostArgs* as, int engines, int nro, int npre,
+                       hipStream_t s);
+int weights_group_tiles(int J, int N, int K_loc);
+void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K_loc, hipStream_t s);
+void launch_update_group(int J, int N, const UpdateArgs* as, int engines, hipStream_t s);
 void launch_gather_max(const double* gathered, int world, int n, double* out, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);

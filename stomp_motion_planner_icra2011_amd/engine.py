@@ -89,7 +89,9 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
             "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id",
             "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
-            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_sdf_build_objects"]
+            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_sdf_build_objects",
+            "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
+            "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy"]
 
 _lib = None
 
@@ -137,6 +139,14 @@ def load_library(path: Optional[str] = None):
     l.stomp_sdf_build_objects.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double,
                                           C.POINTER(stomp_shape), C.c_int32, dp, C.c_int64, C.c_void_p,
                                           C.POINTER(C.c_int64), C.c_void_p]
+    l.stomp_stream_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
+    l.stomp_stream_destroy.argtypes = [C.c_void_p]
+    l.stomp_group_create.argtypes = [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p)]
+    l.stomp_group_run.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+    l.stomp_group_synchronize.argtypes = [C.c_void_p]
+    l.stomp_group_last_error.restype = C.c_char_p
+    l.stomp_group_last_error.argtypes = [C.c_void_p]
+    l.stomp_group_destroy.argtypes = [C.c_void_p]
     l.stomp_comm_unique_id.argtypes = [C.c_void_p]
     l.stomp_comm_local_id.argtypes = [C.c_int32, C.c_void_p]
     l.stomp_device_alloc.argtypes = [C.c_int32, C.c_uint64, C.POINTER(C.c_void_p)]
@@ -407,6 +417,58 @@ class Engine:
         t, n = C.c_double(), C.c_int32()
         _check(load_library().stomp_engine_get_timing(self.h, name.encode(), C.byref(t), C.byref(n)), self.h)
         return t.value, n.value
+
+
+class Stream:
+    """A HIP stream of the engine runtime (engines of one group share one)."""
+
+    def __init__(self, device: int = 0):
+        self.ptr = None
+        p = C.c_void_p()
+        _check(load_library().stomp_stream_create(device, C.byref(p)))
+        self.ptr = p.value
+
+    def close(self):
+        if self.ptr:
+            load_library().stomp_stream_destroy(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+
+class EngineGroup:
+    """Engines of one shape on one shared stream, advanced in lockstep by shared launches
+    (stomp_group_run: three dispatches per iteration for the whole group)."""
+
+    def __init__(self, engines):
+        self._h = None   # set before the call that may raise, so __del__ has nothing to free
+        l = load_library()
+        self.engines = list(engines)
+        arr = (C.c_void_p * len(self.engines))(*[e.h.value for e in self.engines])
+        h = C.c_void_p()
+        rc = l.stomp_group_create(arr, len(self.engines), C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"stomp group error {rc}: {l.stomp_last_error().decode()}")
+        self._h = h
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(f"stomp group error {rc}: {load_library().stomp_group_last_error(self._h).decode()}")
+
+    def run(self, first: int, count: int):
+        self._check(load_library().stomp_group_run(self._h, first, count))
+
+    def synchronize(self):
+        self._check(load_library().stomp_group_synchronize(self._h))
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            load_library().stomp_group_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 class DeviceBuffer:
