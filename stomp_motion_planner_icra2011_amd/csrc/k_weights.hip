@@ -491,6 +491,19 @@ bool weights_carry_pregen(int K_loc)
 #endif
 }
 
+// half-width row tiles for K_loc in (32 RS, 64 RS]: two flat columns per workgroup, so a lane's
+// 32 rows still fit its registers (the whole K = 4096 of cfg3 on one device; the one-column
+// k_weights tiles read a separate line per row there)
+template <int EPT>
+static void launch_rows2(const WeightArgs& a, hipStream_t s)
+{
+    constexpr int TCW = 2;
+    const int nw = (a.J * a.N + TCW - 1) / TCW;
+    const size_t lds = weights_rows_v_bytes(a.K_loc, TCW);
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows<TCW, EPT>, lds);
+    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(kWRB), lds, s, a);
+}
+
 void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre)
 {
 #ifndef WEIGHTS_COLUMN_TILES
@@ -503,6 +516,7 @@ void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre)
         if (a.K_loc <= 16 * RS) return launch_rows<16>(a, pre, s);
         if (a.K_loc <= 32 * RS) return launch_rows<32>(a, pre, s);
     }
+    if (!pre && kWRB == 256 && nb * 2 <= kWRB && a.K_loc <= 32 * (kWRB / 2)) return launch_rows2<32>(a, s);
 #endif
     if (pre) launch_pregen(*pre, pre->K_loc, s);   // not reached: the engine checks weights_carry_pregen
     dim3 grid((a.N + a.tc - 1) / a.tc, a.J);

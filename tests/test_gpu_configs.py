@@ -136,6 +136,20 @@ def test_cfg3_whole_iteration_on_one_device(sdf256_n199, monkeypatch, sharded):
     np.testing.assert_array_equal(e.rollouts("params"), o.rollouts("params"))
 
 
+@pytest.mark.parametrize("K,reused", [(2049, 0), (3001, 300)])
+def test_half_width_weights_tiles_bitwise(sdf256_n199, K, reused):
+    # K in (2048, 4096]: the weights update runs the two-column row tiles (ragged K, with and
+    # without reuse), every rollout field bit for bit
+    base, buf = sdf256_n199
+    p = pb.make_problem(dof=7, waypoints=100, grid_n=256, num_rollouts=K, num_reused_rollouts=reused,
+                        build_grid=False)
+    p.sdf = base.sdf
+    o = po.Oracle(p, threads=THREADS)
+    e = eng.Engine(p, sdf_device_ptr=buf.ptr)
+    for it in range(1, 4):
+        compare_iteration(o, e, it)
+
+
 def test_cfg4_dual_arm_512_grid_bitwise():
     p, buf = problem_on_device_sdf(dof=14, waypoints=100, grid_n=512, num_rollouts=1024, num_reused_rollouts=0)
     try:
