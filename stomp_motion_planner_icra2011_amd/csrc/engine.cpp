@@ -1152,6 +1152,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || cus <= 0)
             cus = 256;
+        m.cus = cus;
         const int need = (e->K_loc + 1 + cus - 1) / cus;
         m.pad_lds = (with_pad <= kRolloutLdsMax &&
                      rollout_blocks_per_cu(with_pad) >= std::min(need, rollout_blocks_per_cu(without))) ? 1 : 0;

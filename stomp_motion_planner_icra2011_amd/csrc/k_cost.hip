@@ -35,7 +35,19 @@ constexpr int kBlock = ROLLOUT_BLOCK;
 #ifndef ROLLOUT_MIN_WAVES
 #define ROLLOUT_MIN_WAVES (ROLLOUT_BLOCK > 256 ? 4 : 3)
 #endif
-constexpr int kCopyBatch = 12 * 256 / kBlock;   // table-image words per lane per copy pass
+// the wide rollout workgroup: when a launch's rollouts fit one per CU (the K-sharded ranks,
+// the deferred noiseless rollout, small K) no CU runs two of them, so a rollout gets 512
+// lanes (twice the pair lanes per slot round, half the gather rounds per lane) and the
+// register budget of two waves per SIMD
+#ifndef ROLLOUT_WIDE_BLOCK
+#define ROLLOUT_WIDE_BLOCK 512
+#endif
+constexpr int kWideBlock = ROLLOUT_WIDE_BLOCK;
+template <int BLOCK>
+constexpr int rollout_min_waves()
+{
+    return BLOCK == kBlock ? ROLLOUT_MIN_WAVES : (BLOCK > 512 ? 4 : 2);
+}
 #ifndef SPHERE_UNROLL
 #define SPHERE_UNROLL 2
 #endif
@@ -159,6 +171,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     double* zB = (double*)(lds_raw + L.nzB);
     const bool gen = a.fused_noise == 1 && !extra;
     const bool pre = a.fused_noise == 2 && !extra;
+    constexpr int kCopyBatch = 12 * 256 / BLOCK;   // table-image words per lane per copy pass
     unsigned long long img[kCopyBatch];
     const int nw = m.img_words;
 #pragma unroll
@@ -551,7 +564,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 }
 
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m, CostArgs a)
+__global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
     rollout_body<BLOCK>(m, a, blockIdx.x);
 }
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout(DevModel m
 // pregen blocks (npre each, at the default priority behind them all); models and arguments
 // live in device memory, one entry per engine
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, ROLLOUT_MIN_WAVES) void k_rollout_group(const DevModel* ms, const CostArgs* as,
+__global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_group(const DevModel* ms, const CostArgs* as,
                                                                            int engines, int nro, int npre)
 {
     const int b = blockIdx.x;
@@ -615,6 +628,12 @@ void launch_cost_group(const DevModel& m0, const DevModel* ms, const CostArgs* a
     const int blocks = engines * (nro + npre);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m0, m0.pad_lds);
+    if (kWideBlock != kBlock && engines * nro <= m0.cus) {   // e.g. the grouped noiseless flush
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kWideBlock>, lds);
+        hipLaunchKernelGGL((k_rollout_group<kWideBlock>), dim3(blocks), dim3(kWideBlock), lds, s, ms, as, engines, nro,
+                           npre);
+        return;
+    }
     if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kBlock>, lds);
     hipLaunchKernelGGL((k_rollout_group<kBlock>), dim3(blocks), dim3(kBlock), lds, s, ms, as, engines, nro, npre);
 }
@@ -655,9 +674,15 @@ int rollout_blocks_per_cu(size_t lds_total)
 
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
-    const int blocks = a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0);
+    const int nro = a.num_noisy + (a.x_params ? 1 : 0);
+    const int blocks = nro + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
+    if (kWideBlock != kBlock && nro <= m.cus) {
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock>, lds);
+        hipLaunchKernelGGL((k_rollout<kWideBlock>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);
+        return;
+    }
     if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock>, lds);
     hipLaunchKernelGGL((k_rollout<kBlock>), dim3(blocks), dim3(kBlock), lds, s, m, a);
 }

@@ -62,6 +62,8 @@ struct DevModel {
     int nsaves;                 // saved branch-point frames the FK program uses (0..kSaves, LDS)
     int pad_lds;                // padding-row positions staged in LDS (1) or read from HBM (0)
     int sincos_pre;             // every (sin, cos) of the joint-limited trajectory made before the FK
+    int cus;                    // compute units of the device (launch_cost: wide workgroups when a
+                                // launch's rollouts fit one per CU)
                                 // program by all lanes: sines over traj, cosines in the saved-frame
                                 // area (the program's first save comes after its last joint segment)
     const unsigned long long* img;   // the rollout kernel's LDS table image (RolloutLds from .sph on)
