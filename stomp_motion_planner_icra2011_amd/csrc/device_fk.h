@@ -144,7 +144,11 @@ __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* _
     const bool ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
     const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
     const unsigned idx = (unsigned)(ok ? cell : 0.0);
+#ifdef SDF_GATHER_PROBE   // diagnostic only (wrong values): every gather in one line
+    const float v = m.sdf[idx & 31u];
+#else
     const float v = m.sdf[idx];
+#endif
     return ok ? v : 0.0f;
 }
 #elif defined(SDF_TRUNC_ROUND)

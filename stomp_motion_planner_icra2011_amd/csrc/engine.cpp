@@ -1157,6 +1157,11 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         m.pad_lds = (with_pad <= kRolloutLdsMax &&
                      rollout_blocks_per_cu(with_pad) >= std::min(need, rollout_blocks_per_cu(without))) ? 1 : 0;
         const size_t lds = rollout_lds_bytes(m, m.pad_lds) + stat;
+        m.phased_lds = (int)rollout_phased_lds_bytes(m);
+#ifdef NO_PHASED_ROLLOUT
+        m.phased_lds = 0;
+#endif
+        if (getenv("STOMP_DEBUG_PHASED")) fprintf(stderr, "stomp: phased rollout LDS %d B\n", m.phased_lds);
         if (lds > kRolloutLdsMax)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
                                                     "on one segment), more than %zu", lds, J, N, e->S, m.sph_chunk,

@@ -113,14 +113,14 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x)
 
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
-template <int BLOCK>
+template <int BLOCK, bool PHASED = false>
 __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ int flag;
     __shared__ int nz_count;
     const int J = m.J, N = m.N, S = m.S;
-    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
+    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds, PHASED);
     {
         // blocks past the rollouts: the next iteration's pregen rows (normals, sigma L z,
         // M eps), left at the default wave priority while the rollout waves raise theirs, so
@@ -360,6 +360,109 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         }
         __syncthreads();
     }
+    if constexpr (PHASED) {
+        // ---- the phased evaluation (one workgroup per CU): the FK lanes run the whole program
+        // and leave every sphere slot's frame in LDS; then every (sphere, waypoint) pair at once
+        // (one round of gathers), the velocities of the non-zero pairs, and the fold over all
+        // spheres in list order.  Same expressions, same order per waypoint as the slot loop.
+        __builtin_amdgcn_s_setprio(3);
+        if (fk_lane) {
+            for (int op = 0; op < m.nops; ++op) {
+                const FkOp o = ops_s[op];
+                fk_op(o);
+                if (o.slot >= 0) {
+                    double* dst = fb + (size_t)o.slot * 12 * N + t_own;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) dst[k * N] = C.R[k];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
+                }
+                if (op < 40) STAMP(100 + op);
+            }
+        }
+        __builtin_amdgcn_s_setprio(2);
+        if (tid == 0) nz_count = 0;
+        __syncthreads();   // every slot's frame published
+        STAMP(10);
+        // lane (g, t): spheres [g CPL, (g + 1) CPL) at waypoint t, contiguous so that a lane's
+        // spheres mostly share a frame; kLaneSpheres lookups with their gathers in flight at once
+        const int CPL = (S + G - 1) / G;
+        if (pg < G) {
+            double F[12];
+            int fslot = -1;
+            for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
+                float dv[kLaneSpheres];
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    if (u0 + u >= CPL) break;   // uniform
+                    const int sc = min(pg * CPL + u0 + u, S - 1);
+                    const DevSphere& sp = sph[sc];
+                    if (sp.slot != fslot) {
+                        fslot = sp.slot;
+                        const double* src = fb + (size_t)fslot * 12 * N + pt;
+#pragma unroll
+                        for (int k = 0; k < 12; ++k) F[k] = src[k * N];
+                    }
+                    double x[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+                        x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
+                    dv[u] = sdf_distance(m, x);
+                }
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    if (u0 + u >= CPL) break;   // uniform
+                    const int sq = pg * CPL + u0 + u;
+                    const bool in = sq < S;
+                    double pot = 0.0;
+                    if (in) {
+                        const DevSphere& sp = sph[sq];
+                        const double dd = (double)dv[u];
+                        col |= dd <= sp.radius;
+                        pot = potential(sp, dd);
+                        av[sq * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                    }
+                    const bool nz = in && pot != 0.0;
+                    const unsigned long long mask = __ballot(nz);
+                    if (mask) {
+                        const int lane_id = tid & 63;
+                        const int leader = __ffsll((long long)mask) - 1;
+                        int base = 0;
+                        if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                        base = __shfl(base, leader, 64);
+                        if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(sq * N + pt);
+                    }
+                }
+            }
+        }
+        __syncthreads();   // pots and the non-zero list complete
+        STAMP(11);
+        __builtin_amdgcn_s_setprio(3);
+        for (int i = tid; i < nz_count; i += BLOCK) {
+            const int it = nzl[i];
+            const int qi = it / N, ti = it - qi * N;
+            const DevSphere& sp = sph[qi];
+            av[it] *= sphere_speed(m, fb + (size_t)sp.slot * 12 * N, pad, sp, qi, ti);
+        }
+        __syncthreads();   // every a value complete
+        STAMP(12);
+        if (fk_lane) {
+            // fold in sphere order; the LDS reads go out 16 at a time
+            for (int q0 = 0; q0 < S; q0 += 16) {
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, S - 1) * N + t_own];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (q0 + q >= S) break;
+                    cum += v[q];
+                    state += cum;
+                }
+            }
+        }
+        __builtin_amdgcn_s_setprio(2);
+        STAMP(13);
+    } else {
     // the FK chain and the ordered fold run on two waves while the other waves wait at the
     // next barrier: they are this workgroup's critical path, so they take issue priority (3)
     // over the co-resident workgroup's wide, VALU-heavy pair and velocity phases (2) and the
@@ -529,6 +632,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         STAMP(13 + 4 * run);
         ++run;
     }
+    }
     STAMP(4);
     if (col) flag = 1;   // every writer stores 1
     __syncthreads();     // folds done (av reused below), flag complete
@@ -567,6 +671,12 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
     rollout_body<BLOCK>(m, a, blockIdx.x);
+}
+
+// the phased evaluation for launches whose rollouts run one per CU (LDS: rollout_lds phased)
+__global__ __launch_bounds__(kWideBlock, kWideBlock > 512 ? 4 : 2) void k_rollout_phased(DevModel m, CostArgs a)
+{
+    rollout_body<kWideBlock, true>(m, a, blockIdx.x);
 }
 
 // one launch for the rollouts of a group of engines of one shape (stomp_group_run): every
@@ -648,6 +758,16 @@ size_t rollout_lds_bytes(const DevModel& m, int pad_lds)
     return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, pad_lds).total;
 }
 
+size_t rollout_phased_lds_bytes(const DevModel& m)
+{
+    const size_t dyn = rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds, true).total;
+    hipFuncAttributes attr;
+    size_t stat = 2048;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout_phased) == hipSuccess) stat = attr.sharedSizeBytes;
+    if ((size_t)m.S * m.N > 65535 || dyn + stat > kLdsPerCu) return 0;   // pair ids are 16-bit
+    return dyn;
+}
+
 size_t rollout_static_lds()
 {
     hipFuncAttributes attr;
@@ -678,6 +798,12 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     const int blocks = nro + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
+    if (kWideBlock != kBlock && nro <= m.cus && m.phased_lds > 0) {
+        const size_t lp = m.phased_lds;
+        lds_opt_in((const void*)k_rollout_phased, lp);
+        hipLaunchKernelGGL(k_rollout_phased, dim3(blocks), dim3(kWideBlock), lp, s, m, a);
+        return;
+    }
     if (kWideBlock != kBlock && nro <= m.cus) {
         if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock>, lds);
         hipLaunchKernelGGL((k_rollout<kWideBlock>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);

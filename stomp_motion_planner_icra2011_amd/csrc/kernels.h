@@ -62,10 +62,12 @@ struct DevModel {
     int nsaves;                 // saved branch-point frames the FK program uses (0..kSaves, LDS)
     int pad_lds;                // padding-row positions staged in LDS (1) or read from HBM (0)
     int sincos_pre;             // every (sin, cos) of the joint-limited trajectory made before the FK
-    int cus;                    // compute units of the device (launch_cost: wide workgroups when a
-                                // launch's rollouts fit one per CU)
                                 // program by all lanes: sines over traj, cosines in the saved-frame
                                 // area (the program's first save comes after its last joint segment)
+    int cus;                    // compute units of the device (launch_cost: wide workgroups when a
+                                // launch's rollouts fit one per CU)
+    int phased_lds;             // dynamic LDS of the phased wide rollout (every slot's frame and every
+                                // sphere's a value resident), 0 when it does not fit a CU
     const unsigned long long* img;   // the rollout kernel's LDS table image (RolloutLds from .sph on)
     int img_words;              // 8-byte words of it copied to LDS (up to .pad, or .total with pad_lds)
     const DevSegment* segs;
@@ -97,17 +99,21 @@ struct RolloutLds {
     size_t traj, fb, sv, av, nzl, nzA, nzB, sph, seg, ops, slot, hl, jlim, pad, total;
 };
 
+// The phased layout (k_rollout_phased): fb holds every slot's frame [nslots][12][N], av every
+// sphere's a values [S][N] and nzl every pair; the rest as above.
+
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 __host__ __device__ inline int noise_jp(int J) { return (J + kNoiseJT - 1) / kNoiseJT * kNoiseJT; }
 
 __host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_slot, int nsaves, int nseg, int nops,
-                                                  int nslots, int pad_lds)
+                                                  int nslots, int pad_lds, bool phased = false)
 {
     RolloutLds l;
+    if (phased) max_slot = S;
     l.traj = 0;
     l.fb = l.traj + (size_t)J * N * sizeof(double);
-    l.sv = l.fb + (size_t)12 * N * sizeof(double);
+    l.sv = l.fb + (size_t)(phased ? nslots : 1) * 12 * N * sizeof(double);
     l.av = l.sv + (size_t)nsaves * 12 * N * sizeof(double);
     l.nzl = l.av + (size_t)max_slot * N * sizeof(double);
     // noise phase: A = z then x (padded), B = eps then the control-cost terms
@@ -289,6 +295,7 @@ void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, cons
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);
 size_t rollout_lds_bytes(const DevModel& m, int pad_lds);   // dynamic LDS of the rollout kernel
+size_t rollout_phased_lds_bytes(const DevModel& m);        // of the phased wide rollout, 0: does not fit
 size_t rollout_static_lds();                                 // its static LDS
 int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS and register limits)
 // LDS per CU is 160 KiB (MI355X_MICROARCH.md), but three 49.5 KB rollout workgroups did not

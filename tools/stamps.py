@@ -51,6 +51,8 @@ def show(name, block, labels):
 def cost_label(i):
     if i in (61, 62, 63):
         return {61: "control terms (thread 0)", 62: "control terms barrier", 63: "control costs stored (t0)"}[i]
+    if 100 <= i < 140:
+        return f"FK op {i - 100}"
     if 40 <= i < 100:
         return f"slot {i - 40}: gathers issued (last round)"
     if 10 <= i < 40:
