@@ -77,6 +77,63 @@ void launch_pad_fk(const DevModel& m, const double* start, const double* goal, d
 }
 
 // ============================================================== rollout reuse
+// Rollout::getCost (policy_improvement.cpp:149-156) as the reference sums it: the state costs
+// t-ascending, each joint's control costs t-ascending, then s += joint d for d ascending.  The
+// J + 1 t-chains are independent, so each is one lane's (loads two 16-batches ahead of its adds)
+// and only the J final adds are serial: a candidate's total costs ~N + J dependent adds instead
+// of (J + 1) N dependent loads.
+__device__ __forceinline__ double chain_sum(const double* __restrict__ v, int N)
+{
+    double x = v[0];
+    int t = 1;
+    double b[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) b[u] = v[min(t + u, N - 1)];
+    for (; t + 16 <= N; t += 16) {
+        double nb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) nb[u] = v[min(t + 16 + u, N - 1)];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x += b[u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) b[u] = nb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+        if (t + u < N) x += b[u];
+    return x;
+}
+
+constexpr int kReusePart = 2048;   // chain sums staged in LDS per pass (doubles)
+
+// totals of candidates [c0, c1) (c == K: the extra rollout) into out[c - c0]; every thread of
+// the block takes part, `part` is kReusePart doubles of LDS
+__device__ __forceinline__ void reuse_totals_block(int c0, int c1, int K, int J, int N, const double* state,
+                                                   const double* control, const double* x_state,
+                                                   const double* x_control, double* out, double* part)
+{
+    const int L = J + 1, per = kReusePart / L;
+    const size_t JN = (size_t)J * N;
+    for (int a = c0; a < c1; a += per) {
+        const int b = min(c1, a + per);
+        for (int it = threadIdx.x; it < (b - a) * L; it += blockDim.x) {
+            const int c = a + it / L, j = it % L;
+            const double* v;
+            if (j == 0) v = c < K ? state + (size_t)c * N : x_state;
+            else v = (c < K ? control + (size_t)c * JN : x_control) + (size_t)(j - 1) * N;
+            part[it] = chain_sum(v, N);
+        }
+        __syncthreads();
+        for (int c = a + threadIdx.x; c < b; c += blockDim.x) {
+            const double* q = part + (size_t)(c - a) * L;
+            double s = q[0];
+            for (int d = 0; d < J; ++d) s += q[1 + d];
+            out[c - c0] = s != s ? __builtin_inf() : s;   // NaN ranks last: the ranks stay a permutation
+        }
+        __syncthreads();
+    }
+}
+
 // PolicyImprovement::generateRollouts reuse branch (policy_improvement.cpp:176-225): rank the
 // K previous rollouts and the extra (noiseless) rollout by Rollout::getCost (:149-156),
 // lexicographic on (cost, index) with the extra rollout at index -1 (std::sort of pairs), copy
@@ -89,24 +146,13 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
 {
     if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
+    __shared__ double part[kReusePart];
     const int n = K + with_extra;
     double* costs = sh;
     int* sel = (int*)(sh + n);
     const int tid = threadIdx.x, bs = blockDim.x;
     const size_t JN = (size_t)J * N;
-    for (int c = tid; c < n; c += bs) {
-        const double* st = c < K ? state + (size_t)c * N : x_state;
-        const double* ct = c < K ? control + (size_t)c * JN : x_control;
-        double s = st[0];
-        for (int t = 1; t < N; ++t) s += st[t];
-        for (int d = 0; d < J; ++d) {
-            double x = ct[(size_t)d * N];
-            for (int t = 1; t < N; ++t) x += ct[(size_t)d * N + t];
-            s += x;
-        }
-        costs[c] = s != s ? __builtin_inf() : s;   // NaN ranks last: the ranks stay a permutation
-    }
-    __syncthreads();
+    reuse_totals_block(0, n, K, J, N, state, control, x_state, x_control, costs, part);
     for (int c = tid; c < n; c += bs) {
         const int ic = c < K ? c : -1;
         const double cc = costs[c];
@@ -163,17 +209,7 @@ void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double
 // [Kr][J N + N] buffer, the slots are all-gathered and every rank unpacks the reused rows it owns
 // (rows K_gen + r, noise re-based on theta, :214-223).  Same ranking, same row order, so the result
 // is the single-device one bit for bit.
-__device__ __forceinline__ double rollout_total(const double* st, const double* ct, int J, int N)
-{
-    double s = st[0];
-    for (int t = 1; t < N; ++t) s += st[t];
-    for (int d = 0; d < J; ++d) {
-        double x = ct[(size_t)d * N];
-        for (int t = 1; t < N; ++t) x += ct[(size_t)d * N + t];
-        s += x;
-    }
-    return s != s ? __builtin_inf() : s;   // NaN ranks last (as k_reuse)
-}
+constexpr int kReuseTotalsPerBlock = 64;   // candidates per k_reuse_totals block (reuse_totals_block)
 
 __global__ __launch_bounds__(256) void k_reuse_totals(int K_loc, int J, int N, const double* state,
                                                       const double* control, const double* x_state,
@@ -181,10 +217,14 @@ __global__ __launch_bounds__(256) void k_reuse_totals(int K_loc, int J, int N, c
                                                       const int* stop)
 {
     if (stop && *stop) return;
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    const size_t JN = (size_t)J * N;
-    if (c < K_loc) tot_loc[c] = rollout_total(state + (size_t)c * N, control + (size_t)c * JN, J, N);
-    else if (c == K_loc) *tot_x = rollout_total(x_state, x_control, J, N);
+    __shared__ double part[kReusePart];
+    __shared__ double tot[kReuseTotalsPerBlock];
+    const int c0 = blockIdx.x * kReuseTotalsPerBlock, c1 = min(K_loc + 1, c0 + kReuseTotalsPerBlock);
+    reuse_totals_block(c0, c1, K_loc, J, N, state, control, x_state, x_control, tot, part);
+    for (int c = c0 + threadIdx.x; c < c1; c += 256) {
+        if (c < K_loc) tot_loc[c] = tot[c - c0];
+        else *tot_x = tot[c - c0];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_reuse_select(int K, int Kr, int with_extra, const double* tot_all,
@@ -248,7 +288,8 @@ __global__ __launch_bounds__(256) void k_reuse_unpack(int Kr, int K_gen, int J, 
 void launch_reuse_totals(int K_loc, int J, int N, const double* state, const double* control, const double* x_state,
                          const double* x_control, double* tot_loc, double* tot_x, const int* stop, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_reuse_totals, dim3((K_loc + 1 + 255) / 256), dim3(256), 0, s, K_loc, J, N, state, control,
+    hipLaunchKernelGGL(k_reuse_totals, dim3((K_loc + 1 + kReuseTotalsPerBlock - 1) / kReuseTotalsPerBlock), dim3(256), 0,
+                       s, K_loc, J, N, state, control,
                        x_state, x_control, tot_loc, tot_x, stop);
 }
 
