@@ -116,6 +116,11 @@ struct stomp_engine {
     std::vector<void*> allocs;
     double *d_theta = nullptr, *d_LT = nullptr, *d_MT = nullptr, *d_QT = nullptr;
     double *d_params = nullptr, *d_noise = nullptr, *d_control = nullptr, *d_prob = nullptr, *d_state = nullptr;
+    // K_r > 0: a second set of rollout rows.  Each reusing iteration swaps the sets, so the
+    // previous iteration's rows (ranked and copied by the reuse kernels) stay intact while this
+    // iteration's rollout launch writes its generated rows; row_set counts the swaps mod 2
+    double *d_params_b = nullptr, *d_noise_b = nullptr, *d_control_b = nullptr, *d_state_b = nullptr;
+    int row_set = 0;
     double *d_cum = nullptr, *d_u = nullptr;
     double *d_x_params = nullptr, *d_x_noise = nullptr, *d_x_control = nullptr, *d_x_state = nullptr;
     double *d_last_traj = nullptr, *d_best_traj = nullptr, *d_total = nullptr;
@@ -619,36 +624,63 @@ NoiseArgs pregen_args(const stomp_engine* e, int it)
 // K_gen.. with their noise re-based on the current theta, and generate the rest.  With the rows
 // sharded over ranks the ranking runs on all-gathered totals and the chosen rows travel in slots
 // (k_misc.hip), so every rank ends with exactly its rows of the single-device result.
-int begin_generate(stomp_engine* e)
+void swap_row_sets(stomp_engine* e)
+{
+    std::swap(e->d_params, e->d_params_b);
+    std::swap(e->d_noise, e->d_noise_b);
+    std::swap(e->d_control, e->d_control_b);
+    std::swap(e->d_state, e->d_state_b);
+    e->row_set ^= 1;
+}
+
+// generateRollouts' bookkeeping: K_gen, and whether the reuse step runs this iteration; when it
+// does the row sets swap, so the previous rows are the reuse source (d_*_b) and this iteration's
+// rows are written into the other set
+bool plan_generate(stomp_engine* e)
 {
     e->K_gen = e->K - e->Kr;
     if (!e->reused_next) {
         e->K_gen = e->K;
         if (e->Kr > 0) e->reused_next = true;
-        return 0;
+        return false;
     }
-    flush_noiseless(e);
+    swap_row_sets(e);
+    return true;
+}
+
+// the reuse step: rank the previous rows and the extra (noiseless) rollout, copy the best K_r
+// into rows K_gen.. of this iteration's set (the extra rollout's state costs must be evaluated)
+int run_reuse(stomp_engine* e)
+{
     Timed tm(e, T_REUSE);
     const int with_extra = e->extra_added ? 1 : 0;
     e->extra_added = false;
     if (e->world == 1) {
-        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params, e->d_noise, e->d_state, e->d_control,
-                     e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta, e->d_tmp_params, e->d_tmp_state,
-                     e->d_stop, e->stream);
+        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
+                     e->d_params, e->d_noise, e->d_state, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta,
+                     e->d_tmp_params, e->d_tmp_state, e->d_stop, e->stream);
         return 0;
     }
     const size_t slot = (size_t)e->Kr * ((size_t)e->J * e->N + e->N);
-    launch_reuse_totals(e->K_loc, e->J, e->N, e->d_state, e->d_control, e->d_x_state, e->d_x_control, e->d_tot_loc,
-                        e->d_tot_x, e->d_stop, e->stream);
+    launch_reuse_totals(e->K_loc, e->J, e->N, e->d_state_b, e->d_control_b, e->d_x_state, e->d_x_control,
+                        e->d_tot_loc, e->d_tot_x, e->d_stop, e->stream);
     int rc = exchange_gather(e, e->d_tot_loc, e->d_tot_all, (size_t)e->K_loc);
     if (rc) return rc;
     launch_reuse_select(e->K, e->Kr, with_extra, e->d_tot_all, e->d_tot_x, e->d_sel, e->d_stop, e->stream);
-    launch_reuse_pack(e->Kr, e->J, e->N, e->first, e->K_loc, e->d_sel, e->d_params, e->d_state, e->d_slot, e->d_stop,
-                      e->stream);
+    launch_reuse_pack(e->Kr, e->J, e->N, e->first, e->K_loc, e->d_sel, e->d_params_b, e->d_state_b, e->d_slot,
+                      e->d_stop, e->stream);
     if ((rc = exchange_gather(e, e->d_slot, e->d_slot_all, slot))) return rc;
     launch_reuse_unpack(e->Kr, e->K_gen, e->J, e->N, e->first, e->K_loc, e->d_sel, e->d_slot_all, e->d_x_params,
                         e->d_x_state, e->d_theta, e->d_params, e->d_noise, e->d_state, e->d_stop, e->stream);
     return 0;
+}
+
+// plan + reuse at once (callers that evaluate no rollouts of their own before the ranking)
+int begin_generate(stomp_engine* e)
+{
+    if (!plan_generate(e)) return 0;
+    flush_noiseless(e);
+    return run_reuse(e);
 }
 
 // One runSingleIteration (policy_improvement_loop.cpp:143-202) enqueued on the engine stream.
@@ -657,23 +689,28 @@ int begin_generate(stomp_engine* e)
 int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
 {
     const int member = it - 1;
-    NoiseArgs na = noise_args(e, it);
-    if (e->Kr > 0) pipelined = false;   // the reuse ranking needs the extra rollout first
-
-    {
-        int rc = begin_generate(e);
-        if (rc) return rc;
-    }
-    na.K_gen_global = e->K_gen;
-    // generated rows [0, g1 - g0) of this shard: their noise is made by the rollout kernel
-    // itself (fused), k_noise only projects and prices the reused rows after them
-    const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
-    const int num_gen = std::max(g1 - g0, 0);
 #ifndef STOMP_SEPARATE_NOISE
     const bool fused = e->J <= 16;   // rollout_project: at most four 4-joint column groups
 #else
     const bool fused = false;
 #endif
+    // With fused noise the reuse step runs after the rollout launch: the generated rows go to
+    // the other row set, and the launch also evaluates the pending noiseless rollout that the
+    // ranking needs (so K_r > 0 iterations pipeline like K_r = 0 ones).  Otherwise k_noise
+    // makes every row before the launch and the reuse step has to come first.
+    if (e->Kr > 0 && !fused) pipelined = false;
+    const bool reuse = plan_generate(e);
+    const bool reuse_late = reuse && fused;
+    if (reuse && !reuse_late) {
+        flush_noiseless(e);
+        if (int rc = run_reuse(e)) return rc;
+    }
+    NoiseArgs na = noise_args(e, it);
+    na.K_gen_global = e->K_gen;
+    // generated rows [0, g1 - g0) of this shard: their noise is made by the rollout kernel
+    // itself (fused), k_noise only projects and prices the reused rows after them
+    const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
+    const int num_gen = std::max(g1 - g0, 0);
     if (fused) na.row_begin = num_gen;
     // every local row generated (K_r = 0): eps and M eps come from k_pregen
     const bool pre = fused && e->pre_on && num_gen == e->K_loc;
@@ -691,7 +728,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         }
         e->pre_it = -1;
     }
-    if (na.row_begin < na.K_loc) {
+    if (na.row_begin < na.K_loc && !reuse_late) {
         Timed tm(e, T_NOISE);
         launch_noise(na, e->stream);
     }
@@ -726,6 +763,15 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         // before this iteration's weights / update: a break decided on the previous
         // iteration's noiseless rollout leaves theta where the reference leaves it
         track_noiseless(e, ca);
+    }
+    if (reuse_late) {
+        // the previous rows and the extra rollout (evaluated just now) ranked; the reused rows'
+        // projection and control costs after them
+        if (int rc = run_reuse(e)) return rc;
+        if (na.row_begin < na.K_loc) {
+            Timed tm(e, T_NOISE);
+            launch_noise(na, e->stream);
+        }
     }
     WeightArgs wa{};
     wa.stop = e->d_stop;
@@ -782,11 +828,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         // it breaks (stomp_optimizer.cpp:293 -> policy_improvement_loop.cpp:192), and the next
         // iteration's reuse ranking reads it.  After a stop theta no longer changes, so the
         // launches of iterations enqueued past it recompute the same row.
-        HIP_TRY(e, hipMemcpyAsync(e->d_x_params, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToDevice,
-                                  e->stream));
         NoiseArgs xa = na;
         xa.stop = nullptr;
-        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 1; xa.row_begin = 0;
+        // zero_noise 2: the launch itself copies theta into x_params (no separate device copy)
+        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 2; xa.row_begin = 0;
         xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
         launch_noise(xa, e->stream);
         e->extra_added = true;
@@ -976,6 +1021,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(dev_alloc(e, &e->d_control, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_prob, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
+    if (e->Kr > 0) {
+        CREATE_TRY(dev_alloc(e, &e->d_params_b, KJN));
+        CREATE_TRY(dev_alloc(e, &e->d_noise_b, KJN));
+        CREATE_TRY(dev_alloc(e, &e->d_control_b, KJN));
+        CREATE_TRY(dev_alloc(e, &e->d_state_b, (size_t)e->K_loc * N));
+    }
     if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
     if (e->split_modes) {
@@ -1434,7 +1485,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     launch_track_start(e->d_track, e->stream);   // stomp_optimizer.cpp:251 start_time
     const int max_it = e->max_it;
     // host-side generateRollouts state after each iteration, to restore the one the device stopped at
-    struct HostState { bool reused_next, extra_added; };
+    struct HostState { bool reused_next, extra_added; int row_set; };
     std::vector<HostState> after((size_t)std::max(max_it, 1));
     const int chunk = 8;
     int next = 0, checked = 0;
@@ -1446,9 +1497,9 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
         for (; next < end; ++next) {
             // K_r = 0: the noiseless rollout of iteration next rides in the next iteration's
             // rollout launch (pipelined), its k_track right after that launch
-            int rc = enqueue_iteration(e, next + 1, e->Kr == 0);
+            int rc = enqueue_iteration(e, next + 1, true);
             if (rc) return rc;
-            after[next] = {e->reused_next, e->extra_added};
+            after[next] = {e->reused_next, e->extra_added, e->row_set};
         }
         HIP_TRY(e, hipMemcpyAsync(&e->h_track[slot], e->d_track, sizeof(DevTrack), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(e, hipEventRecord(ev[slot], e->stream));
@@ -1482,6 +1533,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     if (t.iterations > 0) {
         e->reused_next = after[t.iterations - 1].reused_next;
         e->extra_added = after[t.iterations - 1].extra_added;
+        if (e->row_set != after[t.iterations - 1].row_set) swap_row_sets(e);   // iterations past the stop were no-ops
     }
     if (costs_per_it && t.iterations > 0)
         HIP_TRY(e, hipMemcpy(costs_per_it, e->d_opt_costs, sizeof(double) * t.iterations, hipMemcpyDeviceToHost));

@@ -138,8 +138,9 @@ __device__ __forceinline__ void reuse_totals_block(int c0, int c1, int K, int J,
 // K previous rollouts and the extra (noiseless) rollout by Rollout::getCost (:149-156),
 // lexicographic on (cost, index) with the extra rollout at index -1 (std::sort of pairs), copy
 // the best K_r into rows K_gen.. and re-base their noise on the current theta.
-__global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params,
-                                               double* noise, double* state, const double* control,
+__global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra,
+                                               const double* src_params, const double* src_state,
+                                               const double* control, double* params, double* noise, double* state,
                                                const double* x_params, const double* x_state,
                                                const double* x_control, const double* theta, double* tmp_params,
                                                double* tmp_state, const int* stop)
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
     int* sel = (int*)(sh + n);
     const int tid = threadIdx.x, bs = blockDim.x;
     const size_t JN = (size_t)J * N;
-    reuse_totals_block(0, n, K, J, N, state, control, x_state, x_control, costs, part);
+    reuse_totals_block(0, n, K, J, N, src_state, control, x_state, x_control, costs, part);
     for (int c = tid; c < n; c += bs) {
         const int ic = c < K ? c : -1;
         const double cc = costs[c];
@@ -169,13 +170,13 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
         const int r = (int)(idx / JN);
         const size_t off = idx % JN;
         const int src = sel[r];
-        tmp_params[idx] = src < K ? params[(size_t)src * JN + off] : x_params[off];
+        tmp_params[idx] = src < K ? src_params[(size_t)src * JN + off] : x_params[off];
     }
     for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
         const int r = (int)(idx / N);
         const int t = (int)(idx % N);
         const int src = sel[r];
-        tmp_state[idx] = src < K ? state[(size_t)src * N + t] : x_state[t];
+        tmp_state[idx] = src < K ? src_state[(size_t)src * N + t] : x_state[t];
     }
     __syncthreads();
     for (size_t idx = tid; idx < (size_t)Kr * JN; idx += bs) {
@@ -193,14 +194,15 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
     }
 }
 
-void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,
-                  double* state, const double* control, const double* x_params, const double* x_state,
-                  const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
-                  const int* stop, hipStream_t s)
+void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
+                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
+                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
+                  double* tmp_params, double* tmp_state, const int* stop, hipStream_t s)
 {
     const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
-    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, params, noise, state,
-                       control, x_params, x_state, x_control, theta, tmp_params, tmp_state, stop);
+    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
+                       src_control, params, noise, state, x_params, x_state, x_control, theta, tmp_params, tmp_state,
+                       stop);
 }
 
 // ---- the same reuse step with the K rows sharded over ranks: every rank prices its

@@ -119,7 +119,14 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
         for (int rr = 0; rr < RT; ++rr) {
             const int r = r0 + rr;
             double p = 0.0;
-            if (r < a.K_loc) p = a.params[((size_t)r * J + d) * N + i];
+            if (r < a.K_loc) {
+                if (a.zero_noise == 2) {   // the extra rollout of theta: params = theta, copied here
+                    p = a.theta[(size_t)d * N + i];
+                    a.params[((size_t)r * J + d) * N + i] = p;
+                } else {
+                    p = a.params[((size_t)r * J + d) * N + i];
+                }
+            }
             xs[rr * Nall + i + 6] = p + acc[rr];
         }
     }

@@ -152,7 +152,8 @@ struct NoiseArgs {
     double* params;
     double* noise;
     double* control;
-    int zero_noise;             // extra rollout: params given, noise = 0 (addExtraRollouts)
+    int zero_noise;             // extra rollout: params given, noise = 0 (addExtraRollouts); 2: params
+                                // are theta, copied into params by the launch
     const int* stop;            // device-resident optimize loop: nonzero -> the launch is a no-op
     int row_begin;              // only rows [row_begin, K_loc) (reused rows after the reuse kernel)
     double* pre_eps;            // [K_loc][J][N] eps = sigma L z made ahead of the rollout launch (k_pregen)
@@ -329,10 +330,12 @@ void launch_update_group(int J, int N, const UpdateArgs* as, int engines, hipStr
 void launch_gather_max(const double* gathered, int world, int n, double* out, hipStream_t s);
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);
-void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, double* params, double* noise,
-                  double* state, const double* control, const double* x_params, const double* x_state,
-                  const double* x_control, const double* theta, double* tmp_params, double* tmp_state,
-                  const int* stop, hipStream_t s);
+// src_*: the previous iteration's rows (ranked, copied from); params / noise / state: this
+// iteration's rows K_gen.. (written); the two may be the same buffers
+void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
+                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
+                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
+                  double* tmp_params, double* tmp_state, const int* stop, hipStream_t s);
 // sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
 // noise = eps, params = theta_gen + eps of rows left in a pregen buffer (rows_in_pre)
 void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,
