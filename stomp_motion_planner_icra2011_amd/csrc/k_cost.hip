@@ -197,8 +197,16 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         for (int w = tid + kCopyBatch * BLOCK; w < nw; w += BLOCK) dst[w] = m.img[w];
     }
     STAMP(6);
-    if (gen) rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
-    else if (pre) rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid);
+    // phased with x in the a-value buffers: the control costs are made during the FK program
+    // (not for the split pipeline's preparation launch, which ends before the FK program)
+    const bool defer = PHASED && L.nzA == L.av && (gen || pre) && !a.prep_only;
+    if (gen) {
+        if (defer) rollout_project<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
+        else rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
+    } else if (pre) {
+        if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
+        else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid);
+    }
     if (tid == 0) flag = 0;
     __syncthreads();
     STAMP(1);
@@ -366,6 +374,15 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // (one round of gathers), the velocities of the non-zero pairs, and the fold over all
         // spheres in list order.  Same expressions, same order per waypoint as the slot loop.
         __builtin_amdgcn_s_setprio(3);
+        // the waves without FK lanes price the row (deferred control costs), one joint per wave
+        const int fk_off = t_own - tid;   // -128 or 0
+        const int fk_w0 = -fk_off / 64, fk_w1 = (N - 1 - fk_off) / 64;
+        if (defer && (wv < fk_w0 || wv > fk_w1)) {
+            const int nfk = fk_w1 - fk_w0 + 1;
+            const int cw = wv < fk_w0 ? wv : wv - nfk;
+            for (int d = cw; d < J; d += NW - nfk)
+                wave_control(a.nz, (size_t)e * J * N, zA, zB, d, lane);
+        }
         if (fk_lane) {
             for (int op = 0; op < m.nops; ++op) {
                 const FkOp o = ops_s[op];

@@ -120,6 +120,9 @@ __host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_s
     const size_t nzw = (size_t)(N + kBandBatch) * noise_jp(J) > (size_t)J * (N + 12)
                            ? (size_t)(N + kBandBatch) * noise_jp(J) : (size_t)J * (N + 12);
     l.nzA = l.fb;
+    // phased: in the a-value buffers when they hold both (they are dead until the pairs), so x
+    // and the control terms survive the FK program, which prices the row on its idle waves
+    if (phased && (size_t)S * N * (sizeof(double) + sizeof(unsigned short)) >= 2 * nzw * sizeof(double)) l.nzA = l.av;
     l.nzB = l.nzA + nzw * sizeof(double);
     size_t end = l.nzl + (size_t)max_slot * N * sizeof(unsigned short);
     if (l.nzB + nzw * sizeof(double) > end) end = l.nzB + nzw * sizeof(double);

@@ -285,7 +285,9 @@ __device__ __forceinline__ void mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, in
 template <int BLOCK>
 __device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid);
 
-template <int BLOCK, int NG>
+// DEFER: leave x in zA for wave_control (the phased rollout prices the row on the waves the FK
+// program leaves idle) instead of rollout_control here
+template <int BLOCK, int NG, bool DEFER = false>
 __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                    int tid)
 {
@@ -348,7 +350,49 @@ __device__ __forceinline__ void rollout_project_ng(const NoiseArgs& a, int r, do
             if (i < N && d < J) xs[d * Nall + i + 6] = traj[d * N + i] + acc[g];
         }
     }
-    rollout_control<BLOCK>(a, row, xs, zB, tid);   // eps is dead
+    if (!DEFER) rollout_control<BLOCK>(a, row, xs, zB, tid);   // eps is dead
+}
+
+// rollout_control for joint d by one wave, no block barrier (a wave's LDS accesses execute in
+// program order): the padding, the 7-tap terms of joint d into cs, its control row to HBM.
+// The same expressions as rollout_control.
+__device__ __forceinline__ void wave_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int d, int lane)
+{
+    const int N = a.N, Nall = a.Nall;
+    double* x = xs + d * Nall;
+    double* c = cs + d * Nall;
+    if (lane < 12) x[lane < 6 ? lane : N + lane] = lane < 6 ? a.start[d] : a.goal[d];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int R = kCtlRun;
+    const int nrun = (Nall + R - 1) / R;
+    for (int item = lane; item < nrun; item += 64) {
+        const int ii0 = item * R;
+        double xw[R + 6];
+#pragma unroll
+        for (int q = 0; q < R + 6; ++q) xw[q] = x[min(max(ii0 - 3 + q, 0), Nall - 1)];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const int ii = ii0 + u;
+            double call = 0.0;
+#pragma unroll
+            for (int rule = 0; rule < 3; ++rule) {
+                const double wr = a.wr[rule];
+                if (wr == 0.0) continue;   // adds +0.0 in the reference: exact to skip
+                double sacc = 0.0;
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if (ii - 3 + q >= 0 && ii - 3 + q < Nall) sacc += a.dcoef[rule][q] * xw[u + q];
+                call += wr * (sacc * sacc);
+            }
+            if (ii < Nall) c[ii] = call;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = lane; t < N; t += 64) a.control[row + (size_t)d * N + t] = control_cost(c, N, Nall, t);
 }
 
 // computeControlCosts of one row from xs = the free part of params + M eps at [d][6 + i]
@@ -477,7 +521,7 @@ __device__ __forceinline__ void pregen_meps_ng(const NoiseArgs& a, int r, const 
 
 // the rollout kernel's row from k_pregen's eps and M eps: params = theta + eps into traj (LDS)
 // and HBM, the noise row, x = params + M eps, then the control costs (rollout_control)
-template <int BLOCK>
+template <int BLOCK, bool DEFER = false>
 __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                  int tid)
 {
@@ -510,16 +554,16 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
             }
         }
     }
-    rollout_control<BLOCK>(a, row, xs, zB, tid);
+    if (!DEFER) rollout_control<BLOCK>(a, row, xs, zB, tid);
 }
 
 // the engine runs the fused phase for J <= 16 (at most four groups of 4 joint columns)
-template <int BLOCK>
+template <int BLOCK, bool DEFER = false>
 __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                 int tid)
 {
-    if (a.J <= 8) rollout_project_ng<BLOCK, 2>(a, r, traj, zA, zB, tid);
-    else rollout_project_ng<BLOCK, 4>(a, r, traj, zA, zB, tid);
+    if (a.J <= 8) rollout_project_ng<BLOCK, 2, DEFER>(a, r, traj, zA, zB, tid);
+    else rollout_project_ng<BLOCK, 4, DEFER>(a, r, traj, zA, zB, tid);
 }
 
 }  // namespace stomp
