@@ -652,14 +652,19 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     }
     STAMP(4);
     if (col) flag = 1;   // every writer stores 1
-    __syncthreads();     // folds done (av reused below), flag complete
+    // lane t's cost into av[t], which only lane t's fold reads: one barrier covers the flag and
+    // the costs, and the state-cost stores come after it (a global store before a barrier makes
+    // the barrier wait for its completion)
+    double cost = 0.0;
     if (fk_lane) {
-        const double cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
-        double* so = extra ? a.x_state : a.state_out + (long long)e * N;
-        so[t_own] = cost;
+        cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
         av[t_own] = cost;
     }
     __syncthreads();
+    if (fk_lane) {
+        double* so = extra ? a.x_state : a.state_out + (long long)e * N;
+        so[t_own] = cost;
+    }
     if (tid == 0) {
         const bool cf = !flag && !(member == 0 && m.pad_collision);
         uint8_t* cfo = extra ? a.x_cf : (a.cf_out ? a.cf_out + e : nullptr);
