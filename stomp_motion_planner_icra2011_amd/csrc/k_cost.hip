@@ -176,6 +176,9 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     const int nw = m.img_words;
 #pragma unroll
     for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
+    // the pregen row's first chunk goes out with the image loads (one memory latency for both)
+    PreChunk pc0;
+    if (pre) pre_chunk_load<BLOCK>(a.nz, e, 0, tid, pc0);
     if (gen) {
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
     } else if (!pre) {
@@ -204,8 +207,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         if (defer) rollout_project<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
         else rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
     } else if (pre) {
-        if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
-        else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid);
+        if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
+        else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid, pc0);
     }
     if (tid == 0) flag = 0;
     __syncthreads();

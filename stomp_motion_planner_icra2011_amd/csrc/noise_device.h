@@ -519,24 +519,42 @@ __device__ __forceinline__ void pregen_meps_ng(const NoiseArgs& a, int r, const 
     }
 }
 
+// one lane's share of a 4 BLOCK chunk of k_pregen's row (eps, M eps, theta)
+struct PreChunk {
+    double e[4], mp[4], th[4];
+};
+
+template <int BLOCK>
+__device__ __forceinline__ void pre_chunk_load(const NoiseArgs& a, int r, int idx0, int tid, PreChunk& c)
+{
+    const int JN = a.J * a.N;
+    const size_t row = (size_t)r * JN;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int idx = min(idx0 + tid + u * BLOCK, JN - 1);
+        c.e[u] = a.pre_eps[row + idx];
+        c.mp[u] = a.pre_meps[row + idx];
+        c.th[u] = a.theta[idx];
+    }
+}
+
 // the rollout kernel's row from k_pregen's eps and M eps: params = theta + eps into traj (LDS)
-// and HBM, the noise row, x = params + M eps, then the control costs (rollout_control)
+// and HBM, the noise row, x = params + M eps, then the control costs (rollout_control).  first:
+// chunk 0, loaded by the caller (its loads in flight with the table image's)
 template <int BLOCK, bool DEFER = false>
 __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
-                                                 int tid)
+                                                 int tid, const PreChunk& first)
 {
     const int J = a.J, N = a.N, Nall = a.Nall, JN = J * N;
     const size_t row = (size_t)r * JN;
     double* xs = zA;
     for (int idx0 = 0; idx0 < JN; idx0 += 4 * BLOCK) {
-        double e[4], mp[4], th[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int idx = min(idx0 + tid + u * BLOCK, JN - 1);
-            e[u] = a.pre_eps[row + idx];
-            mp[u] = a.pre_meps[row + idx];
-            th[u] = a.theta[idx];
-        }
+        PreChunk c;
+        if (idx0 == 0) c = first;
+        else pre_chunk_load<BLOCK>(a, r, idx0, tid, c);
+        const double* e = c.e;
+        const double* mp = c.mp;
+        const double* th = c.th;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int idx = idx0 + tid + u * BLOCK;
