@@ -380,6 +380,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // the waves without FK lanes price the row (deferred control costs), one joint per wave
         const int fk_off = t_own - tid;   // -128 or 0
         const int fk_w0 = -fk_off / 64, fk_w1 = (N - 1 - fk_off) / 64;
+        // N <= 256 (cost_supported) puts the FK lanes on at most four of the eight waves
+        static_assert(!PHASED || BLOCK >= 512, "the phased body prices rows on its non-FK waves");
         if (defer && (wv < fk_w0 || wv > fk_w1)) {
             const int nfk = fk_w1 - fk_w0 + 1;
             const int cw = wv < fk_w0 ? wv : wv - nfk;

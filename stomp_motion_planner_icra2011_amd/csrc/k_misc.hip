@@ -200,6 +200,7 @@ void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const 
                   double* tmp_params, double* tmp_state, const int* stop, hipStream_t s)
 {
     const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);   // K in the thousands
     hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
                        src_control, params, noise, state, x_params, x_state, x_control, theta, tmp_params, tmp_state,
                        stop);
