@@ -489,6 +489,8 @@ void track_noiseless(stomp_engine* e, const CostArgs& ca)
                  e->d_best_traj, e->J * e->N, e->stream);
 }
 
+NoiseArgs noise_args(const stomp_engine* e, int it);
+
 // noiseless rollout of the current theta (policy_improvement_loop.cpp:180-182), alone
 void launch_noiseless(stomp_engine* e, int member)
 {
@@ -497,6 +499,10 @@ void launch_noiseless(stomp_engine* e, int member)
     ca.num_noisy = 0;
     ca.x_params = e->d_theta; ca.x_member = member;
     ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+    if (e->Kr > 0) {   // it is also the extra rollout of the next reuse ranking
+        ca.nz = noise_args(e, member + 1);
+        ca.x_ctl = e->d_x_control; ca.x_prm = e->d_x_params; ca.x_nse = e->d_x_noise;
+    }
     {
         Timed tm(e, T_NOISELESS);
         launch_rollouts(e, ca);
@@ -749,6 +755,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
             ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+            if (e->Kr > 0) { ca.x_ctl = e->d_x_control; ca.x_prm = e->d_x_params; ca.x_nse = e->d_x_noise; }
             e->pending_member = -1;
         }
         {
@@ -823,17 +830,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         launch_noiseless(e, member);
     }
     if (e->Kr > 0) {
-        // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0.  Not
-        // gated by the optimize loop's stop flag: the reference prices the extra rollout before
-        // it breaks (stomp_optimizer.cpp:293 -> policy_improvement_loop.cpp:192), and the next
-        // iteration's reuse ranking reads it.  After a stop theta no longer changes, so the
-        // launches of iterations enqueued past it recompute the same row.
-        NoiseArgs xa = na;
-        xa.stop = nullptr;
-        // zero_noise 2: the launch itself copies theta into x_params (no separate device copy)
-        xa.K_loc = 1; xa.first_global = 0; xa.K_gen_global = 0; xa.zero_noise = 2; xa.row_begin = 0;
-        xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
-        launch_noise(xa, e->stream);
+        // addExtraRollouts (policy_improvement.cpp:443-462): params = theta, noise = 0 — the
+        // noiseless rollout of theta, whose workgroup (this iteration's noiseless launch, or the
+        // next rollout launch's extra workgroup) also writes the extra rollout's params / noise /
+        // control rows (x_ctl) before the next reuse ranking reads them
         e->extra_added = true;
     }
     hipError_t st = hipGetLastError();

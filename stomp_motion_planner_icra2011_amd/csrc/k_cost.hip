@@ -183,14 +183,27 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
     } else if (!pre) {
         const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
+        const bool xc = extra && a.x_ctl;   // the extra rollout's rows too (addExtraRollouts)
         for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
             double v[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[u] = prm[min(idx0 + tid + u * BLOCK, J * N - 1)];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (idx0 + tid + u * BLOCK < J * N) traj[idx0 + tid + u * BLOCK] = v[u];
+            for (int u = 0; u < 4; ++u) {
+                const int idx = idx0 + tid + u * BLOCK;
+                if (idx < J * N) {
+                    traj[idx] = v[u];
+                    if (xc) {
+                        // k_noise's zero-noise row: noise +0.0, x = params + (M 0 = +0.0)
+                        a.x_prm[idx] = v[u];
+                        a.x_nse[idx] = 0.0;
+                        const int d = idx / N, i = idx - d * N;
+                        zA[d * m.Nall + i + 6] = v[u] + 0.0;
+                    }
+                }
+            }
         }
+        if (xc) rollout_control<BLOCK>(a.nz, 0, zA, zB, tid, a.x_ctl);
     }
     {
         unsigned long long* dst = (unsigned long long*)(lds_raw + L.sph);

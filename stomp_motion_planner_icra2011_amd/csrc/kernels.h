@@ -190,6 +190,12 @@ struct CostArgs {
     uint8_t* x_cf;
     double* x_traj;
     double* x_total;
+    // K_r > 0: the noiseless rollout is also addExtraRollouts' extra rollout (parameters theta,
+    // noise 0; policy_improvement.cpp:443-462): its workgroup writes the copy of theta, the zero
+    // noise row and the control costs of theta + 0 (k_noise's zero-noise row) when x_ctl is set
+    double* x_ctl;
+    double* x_prm;
+    double* x_nse;
 };
 
 // Buffers of the split evaluation pipeline (k_rollout prep_only -> k_fk -> k_pairs -> k_fold),

@@ -283,7 +283,8 @@ __device__ __forceinline__ void mfma_tile(__amdgpu_buffer_rsrc_t rsrc, int N, in
 }
 
 template <int BLOCK>
-__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid);
+__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid,
+                                                double* ctl = nullptr);
 
 // DEFER: leave x in zA for wave_control (the phased rollout prices the row on the waves the FK
 // program leaves idle) instead of rollout_control here
@@ -399,8 +400,10 @@ __device__ __forceinline__ void wave_control(const NoiseArgs& a, size_t row, dou
 // (written by the caller, not yet synchronised): the padding, the 7-tap terms into cs and the
 // control row to HBM
 template <int BLOCK>
-__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid)
+__device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, double* xs, double* cs, int tid,
+                                                double* ctl)
 {
+    double* out = ctl ? ctl : a.control;   // ctl: the extra rollout's row
     const int J = a.J, N = a.N, Nall = a.Nall;
     for (int idx = tid; idx < J * 12; idx += BLOCK) {
         const int d = idx / 12, k = idx - d * 12;
@@ -448,7 +451,7 @@ __device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, 
             const int d = item / nrun, t0 = (item - d * nrun) * R;
 #pragma unroll
             for (int u = 0; u < R; ++u)
-                if (t0 + u < N) a.control[row + (size_t)d * N + t0 + u] = control_cost(cs + d * Nall, N, Nall, t0 + u);
+                if (t0 + u < N) out[row + (size_t)d * N + t0 + u] = control_cost(cs + d * Nall, N, Nall, t0 + u);
         }
     }
     STAMP(63);
