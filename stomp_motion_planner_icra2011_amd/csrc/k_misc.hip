@@ -166,31 +166,40 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
         if (rank < Kr) sel[rank] = c;
     }
     __syncthreads();
-    for (size_t idx = tid; idx < (size_t)Kr * JN; idx += bs) {
-        const int r = (int)(idx / JN);
-        const size_t off = idx % JN;
-        const int src = sel[r];
-        tmp_params[idx] = src < K ? src_params[(size_t)src * JN + off] : x_params[off];
+    // the kept rows into rows K_gen.. of this iteration's set (the engine's row sets are distinct
+    // buffers, so the reads need no staging copy): four independent loads in flight per lane
+    (void)tmp_params;
+    (void)tmp_state;
+    const double* __restrict__ sp = src_params;
+    const double* __restrict__ ss = src_state;
+    const size_t np = (size_t)Kr * JN;
+    for (size_t i0 = tid; i0 < np; i0 += 4 * (size_t)bs) {
+        double v[4], th[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t idx = min(i0 + (size_t)u * bs, np - 1);
+            const int r = (int)(idx / JN);
+            const size_t off = idx % JN;
+            const int src = sel[r];
+            v[u] = src < K ? sp[(size_t)src * JN + off] : x_params[off];
+            th[u] = theta[off];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t idx = i0 + (size_t)u * bs;
+            if (idx >= np) continue;
+            const int r = (int)(idx / JN);
+            const size_t off = idx % JN;
+            const size_t dst = (size_t)(K_gen + r) * JN + off;
+            params[dst] = v[u];
+            noise[dst] = v[u] - th[u];
+        }
     }
     for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
         const int r = (int)(idx / N);
         const int t = (int)(idx % N);
         const int src = sel[r];
-        tmp_state[idx] = src < K ? src_state[(size_t)src * N + t] : x_state[t];
-    }
-    __syncthreads();
-    for (size_t idx = tid; idx < (size_t)Kr * JN; idx += bs) {
-        const int r = (int)(idx / JN);
-        const size_t off = idx % JN;
-        const size_t dst = (size_t)(K_gen + r) * JN + off;
-        const double p = tmp_params[idx];
-        params[dst] = p;
-        noise[dst] = p - theta[off];
-    }
-    for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
-        const int r = (int)(idx / N);
-        const int t = (int)(idx % N);
-        state[(size_t)(K_gen + r) * N + t] = tmp_state[idx];
+        state[(size_t)(K_gen + r) * N + t] = src < K ? ss[(size_t)src * N + t] : x_state[t];
     }
 }
 
