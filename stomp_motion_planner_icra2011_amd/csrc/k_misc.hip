@@ -172,34 +172,32 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
     (void)tmp_state;
     const double* __restrict__ sp = src_params;
     const double* __restrict__ ss = src_state;
-    const size_t np = (size_t)Kr * JN;
-    for (size_t i0 = tid; i0 < np; i0 += 4 * (size_t)bs) {
-        double v[4], th[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const size_t idx = min(i0 + (size_t)u * bs, np - 1);
-            const int r = (int)(idx / JN);
-            const size_t off = idx % JN;
-            const int src = sel[r];
-            v[u] = src < K ? sp[(size_t)src * JN + off] : x_params[off];
-            th[u] = theta[off];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const size_t idx = i0 + (size_t)u * bs;
-            if (idx >= np) continue;
-            const int r = (int)(idx / JN);
-            const size_t off = idx % JN;
-            const size_t dst = (size_t)(K_gen + r) * JN + off;
-            params[dst] = v[u];
-            noise[dst] = v[u] - th[u];
-        }
-    }
-    for (size_t idx = tid; idx < (size_t)Kr * N; idx += bs) {
-        const int r = (int)(idx / N);
-        const int t = (int)(idx % N);
+    // row by row (no per-element 64-bit division), four independent loads in flight per lane
+    const int jn = (int)JN;
+    for (int r = 0; r < Kr; ++r) {
         const int src = sel[r];
-        state[(size_t)(K_gen + r) * N + t] = src < K ? ss[(size_t)src * N + t] : x_state[t];
+        const double* prow = src < K ? sp + (size_t)src * JN : x_params;
+        const double* srow = src < K ? ss + (size_t)src * N : x_state;
+        double* pd = params + (size_t)(K_gen + r) * JN;
+        double* nd = noise + (size_t)(K_gen + r) * JN;
+        for (int o0 = tid; o0 < jn; o0 += 4 * bs) {
+            double v[4], th[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int o = min(o0 + u * bs, jn - 1);
+                v[u] = prow[o];
+                th[u] = theta[o];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int o = o0 + u * bs;
+                if (o < jn) {
+                    pd[o] = v[u];
+                    nd[o] = v[u] - th[u];
+                }
+            }
+        }
+        for (int t = tid; t < N; t += bs) state[(size_t)(K_gen + r) * N + t] = srow[t];
     }
 }
 
