@@ -44,12 +44,14 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "STOMP iterations/sec (7-DOF, 100 wp, K=512, 256³ SDF) at 1/2/4/8 GPUs"
 
-# BASELINE.json configs[1..4] (configs[0] is the reference's own CPU case, cfg1)
+# BASELINE.json configs[0..4] (configs[0], cfg1, is the reference's own CPU case: K = 20 with
+# 10 reused rollouts)
 WORKLOADS = {
-    "cfg2": dict(dof=7, waypoints=100, rollouts=512, grid=256, problems=1),
-    "cfg3": dict(dof=7, waypoints=200, rollouts=4096, grid=256, problems=1),
-    "cfg4": dict(dof=14, waypoints=100, rollouts=1024, grid=512, problems=1),
-    "cfg5": dict(dof=7, waypoints=100, rollouts=128, grid=256, problems=64),
+    "cfg1": dict(dof=7, waypoints=100, rollouts=20, grid=128, problems=1, reused=10),
+    "cfg2": dict(dof=7, waypoints=100, rollouts=512, grid=256, problems=1, reused=0),
+    "cfg3": dict(dof=7, waypoints=200, rollouts=4096, grid=256, problems=1, reused=0),
+    "cfg4": dict(dof=14, waypoints=100, rollouts=1024, grid=512, problems=1, reused=0),
+    "cfg5": dict(dof=7, waypoints=100, rollouts=128, grid=256, problems=64, reused=0),
 }
 
 
@@ -64,6 +66,7 @@ def parse():
     ap.add_argument("--dof", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--problems", type=int, default=None, help="cfg5: problems of the whole job")
+    ap.add_argument("--reused", type=int, default=None, help="K_r, reused rollouts (cfg1: 10)")
     ap.add_argument("--enqueue-threads", type=int, default=1, help="cfg5: host threads enqueueing the problems")
     ap.add_argument("--group", type=int, default=-1,
                     help="cfg5: problems per engine group (shared launches; -1 = all of a GPU's problems, "
@@ -292,7 +295,8 @@ def main():
     if world > 1 and K % (64 * world) != 0:
         raise SystemExit(f"K={K} must split into whole 64-rollout blocks over {world} GPUs")
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
-                        num_reused_rollouts=0, build_grid=False, max_iterations=args.warmup + 2 * args.steps + 1)
+                        num_reused_rollouts=args.reused, build_grid=False,
+                        max_iterations=args.warmup + 2 * args.steps + 1)
     sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
     eng.sdf_build_device(p, sdf.ptr)
     comm_id = None
@@ -337,10 +341,12 @@ def main():
     # write + read of the fp64 noise per joint (16 J) and the fp64 state cost (8); one k_rollout
     # launch executes the K_loc noisy rollouts of this rank and the deferred noiseless one
     unit_bytes = 4 * S + 16 * p.J + 8
-    bytes_per_launch = (K_loc + 1) * p.N * unit_bytes
+    # with K_r reused rollouts the launch evaluates only the generated ones (and the noiseless)
+    rows_launch = (K_loc - args.reused if world == 1 else K_loc) + 1
+    bytes_per_launch = rows_launch * p.N * unit_bytes
     # the same launch counting every row it writes (noise, params, control: 24 J) and the
     # noiseless rollout's params read (8 J) instead of 16 J
-    bytes_written_rows = K_loc * p.N * (4 * S + 24 * p.J + 8) + p.N * (4 * S + 8 * p.J + 8)
+    bytes_written_rows = (rows_launch - 1) * p.N * (4 * S + 24 * p.J + 8) + p.N * (4 * S + 8 * p.J + 8)
     roofline = None
     if timing.get("rollout_cost", {}).get("launches"):
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
@@ -353,20 +359,21 @@ def main():
                     "traffic": traffic if headline else None,
                     "traffic_uncorrected": traffic_raw if headline else None,
                     "traffic_source": traffic_src if headline else None,
-                    "kernel": "k_rollout", "unit_bytes": unit_bytes, "units_per_launch": (K_loc + 1) * p.N,
+                    "kernel": "k_rollout", "unit_bytes": unit_bytes, "units_per_launch": rows_launch * p.N,
                     "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3),
                     "frac_vs_measured_6290": round(achieved / 6290.0, 5),
-                    "sdf_only_gbs": round((K_loc + 1) * p.N * 4 * S / avg_s / 1e9, 2),
+                    "sdf_only_gbs": round(rows_launch * p.N * 4 * S / avg_s / 1e9, 2),
                     "frac_rows_written_24J": round(bytes_written_rows / avg_s / 1e9 / HBM_PEAK_GBS, 5),
-                    "iteration_bytes": (K + 1) * p.N * unit_bytes,
-                    "iteration_frac": round((K + 1) * p.N * unit_bytes * value / (HBM_PEAK_GBS * 1e9 * world), 5)}
+                    "iteration_bytes": (K - args.reused + 1) * p.N * unit_bytes,
+                    "iteration_frac": round((K - args.reused + 1) * p.N * unit_bytes * value /
+                                            (HBM_PEAK_GBS * 1e9 * world), 5)}
 
     # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
     # the same iterations with the optimizer's bookkeeping, no early stop
     optimize = None
     if args.optimize_steps > 0 and world == 1:
         po_ = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
-                              num_reused_rollouts=0, build_grid=False, max_iterations=args.optimize_steps,
+                              num_reused_rollouts=args.reused, build_grid=False, max_iterations=args.optimize_steps,
                               max_iterations_after_collision_free=args.optimize_steps + 1)
         eo = eng.Engine(po_, device=local_rank, sdf_device_ptr=sdf.ptr)
         eo.optimize()   # warm
@@ -379,7 +386,7 @@ def main():
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         pc = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
-                             num_reused_rollouts=0)
+                             num_reused_rollouts=args.reused)
         cpu = cpu_baseline(pc, args.cpu_seconds)
         cpu_mt = cpu_baseline_all_cores(pc, min(args.cpu_seconds, 8.0))
 
@@ -390,7 +397,7 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (PR2-like arm, shelf+pole scene, device-built SDF; Philox noise)",
             "config": {"workload": f"{workload_name(args)}: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={K} "
-                                   f"({K_loc}/GPU), K_r=0, {args.grid}^3 SDF, S={S} spheres",
+                                   f"({K_loc}/GPU), K_r={args.reused}, {args.grid}^3 SDF, S={S} spheres",
                        "global_rollouts": K, "rollouts_per_gpu": K_loc,
                        "parallelism": f"rollout shard x{world}" + (" (RCCL)" if world > 1 else ""),
                        "rollouts_per_s": round(value * K, 1)},
