@@ -118,17 +118,7 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // nearest cell round((p - origin) * (1/res)); cells with an index < 1 or >= n-1 read 0.
 // Branch-free so a lane's gathers can all be in flight together: an out-of-range lane
 // loads cell 0 and discards it.
-// C round() (halves away from zero) of u >= 0 is trunc(u) + (u - trunc(u) >= 0.5), exactly (the
-// fraction is exact in fp64); for u < 0 that gives a value <= 0, which the range check below
-// rejects just as it rejects round(u) <= 0.  No sign fix-up, no branch.
-__device__ __forceinline__ double round_nonneg(double u)
-{
-    const double t = trunc(u);
-    return t + ((u - t) >= 0.5 ? 1.0 : 0.0);
-}
-
-#if !defined(SDF_LEGACY_ROUND) && !defined(SDF_TRUNC_ROUND)
-// The same cell rule with fewer operations.  With u = (p - o) * (1/res):
+// The cell rule in few operations.  With u = (p - o) * (1/res):
 //   round(u) >= 1      <=>  u >= 0.5
 //   round(u) <= n - 2  <=>  u < n - 1.5        (n - 1.5 is exact)
 // and for u >= 0.5, floor(u + 0.5) == round(u): u + 0.5 is exact below 2^52 except when it
@@ -144,42 +134,9 @@ __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* _
     const bool ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
     const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
     const unsigned idx = (unsigned)(ok ? cell : 0.0);
-#ifdef SDF_GATHER_PROBE   // diagnostic only (wrong values): every gather in one line
-    const float v = m.sdf[idx & 31u];
-#else
-    const float v = m.sdf[idx];
-#endif
-    return ok ? v : 0.0f;
-}
-#elif defined(SDF_TRUNC_ROUND)
-__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
-{
-    const double fx = round_nonneg((p[0] - m.ox) * m.inv_res);
-    const double fy = round_nonneg((p[1] - m.oy) * m.inv_res);
-    const double fz = round_nonneg((p[2] - m.oz) * m.inv_res);
-    const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
-                    fz < (double)(m.nz - 1);
-    // the cell index in fp64 (in range every term is a small integer, so the products and sums
-    // are exact; the index fits 32 bits, checked at engine creation), selected before the one
-    // conversion: no branch; out of range the lane loads cell 0 and discards it
-    const double cell = (fx * m.ny_d + fy) * m.nz_d + fz;
-    const unsigned idx = (unsigned)(ok ? cell : 0.0);
     const float v = m.sdf[idx];
     return ok ? v : 0.0f;
 }
-#else
-__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
-{
-    const double fx = round((p[0] - m.ox) * m.inv_res);
-    const double fy = round((p[1] - m.oy) * m.inv_res);
-    const double fz = round((p[2] - m.oz) * m.inv_res);
-    const bool ok = fx >= 1.0 && fy >= 1.0 && fz >= 1.0 && fx < (double)(m.nx - 1) && fy < (double)(m.ny - 1) &&
-                    fz < (double)(m.nz - 1);
-    const unsigned idx = ok ? ((unsigned)fx * (unsigned)m.ny + (unsigned)fy) * (unsigned)m.nz + (unsigned)fz : 0u;
-    const float v = m.sdf[idx];
-    return ok ? v : 0.0f;
-}
-#endif
 
 // StompCollisionSpace::getCollisionPointPotentialGradient (stomp_collision_space.h:193-228)
 __device__ __forceinline__ double potential(const DevSphere& s, double dist)

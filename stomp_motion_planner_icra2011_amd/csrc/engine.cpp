@@ -124,8 +124,7 @@ struct stomp_engine {
     double *d_cum = nullptr, *d_u = nullptr;
     double *d_x_params = nullptr, *d_x_noise = nullptr, *d_x_control = nullptr, *d_x_state = nullptr;
     double *d_last_traj = nullptr, *d_best_traj = nullptr, *d_total = nullptr;
-    double *d_tmp_params = nullptr, *d_tmp_state = nullptr, *d_pad_pos = nullptr, *d_start = nullptr,
-           *d_goal = nullptr;
+    double *d_pad_pos = nullptr, *d_start = nullptr, *d_goal = nullptr;
     // sharded reuse (world > 1, K_r > 0): per-rank totals, all totals, the extra's total, the
     // chosen rows' slots [Kr][J N + N] and their all-gather [world][Kr][J N + N], the ranking
     double *d_tot_loc = nullptr, *d_tot_all = nullptr, *d_tot_x = nullptr, *d_slot = nullptr, *d_slot_all = nullptr;
@@ -181,11 +180,6 @@ struct stomp_engine {
     TermsModel tq_model{};
     double *d_tq = nullptr, *d_tq_state = nullptr;
     int wall_khz = 0;
-    // split evaluation pipeline (k_rollout prep -> k_fk -> k_pairs -> k_fold); STOMP_SPLIT=0: fused k_rollout
-    bool split = false;
-    int split_rows = 0;                // rows the split buffers hold
-    SplitBufs sbuf{};
-    double* d_traj_lim = nullptr;      // [split_rows][J][N] joint-limited trajectories
     std::shared_ptr<LocalGroup> local;   // in-process exchange group (stomp_comm_local_id), or null
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     double* d_mm_all = nullptr;          // [world][2][J][N] gathered (max, -min) of a local group
@@ -432,36 +426,10 @@ void release(stomp_engine* e)
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
 }
 
-// split-pipeline buffers for `rows` rollouts of one launch (grown on demand; hipFree waits for the device)
-int ensure_split(stomp_engine* e, int rows)
+// Task::execute of a launch's rollouts
+void launch_rollouts(stomp_engine* e, const CostArgs& ca)
 {
-    if (rows <= e->split_rows) return 0;
-    for (void* p : {(void*)e->sbuf.frames, (void*)e->sbuf.aval, (void*)e->sbuf.colf, (void*)e->d_traj_lim}) {
-        if (!p) continue;
-        hipFree(p);
-        e->allocs.erase(std::remove(e->allocs.begin(), e->allocs.end(), p), e->allocs.end());
-    }
-    const size_t R = (size_t)rows, N = (size_t)e->N;
-    int rc;
-    if ((rc = dev_alloc(e, &e->sbuf.frames, R * std::max(e->nslots, 1) * 12 * N))) return rc;
-    if ((rc = dev_alloc(e, &e->sbuf.aval, R * std::max(e->S, 1) * N))) return rc;
-    if ((rc = dev_alloc(e, &e->sbuf.colf, R * std::max(e->model.nruns, 1)))) return rc;
-    if ((rc = dev_alloc(e, &e->d_traj_lim, R * e->J * N))) return rc;
-    e->split_rows = rows;
-    return 0;
-}
-
-// Task::execute of a launch's rollouts: the fused k_rollout, or the split pipeline
-void launch_rollouts(stomp_engine* e, CostArgs ca)
-{
-    if (!e->split) {
-        launch_cost(e->model, ca, e->stream);
-        return;
-    }
-    const int rows = ca.num_noisy + (ca.x_params ? 1 : 0);
-    if (ensure_split(e, std::max(rows, 1))) return;   // leaves the error; the caller's hipGetLastError is clean
-    if (!ca.traj_out) ca.traj_out = e->d_traj_lim;
-    launch_split_eval(e->model, ca, e->sbuf, e->stream);
+    launch_cost(e->model, ca, e->stream);
 }
 
 // the state-cost terms after the collision cost (k_terms), on the rollouts a k_rollout
@@ -662,9 +630,10 @@ int run_reuse(stomp_engine* e)
     const int with_extra = e->extra_added ? 1 : 0;
     e->extra_added = false;
     if (e->world == 1) {
-        launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
-                     e->d_params, e->d_noise, e->d_state, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta,
-                     e->d_tmp_params, e->d_tmp_state, e->d_stop, e->stream);
+        if (launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
+                         e->d_params, e->d_noise, e->d_state, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta,
+                         e->d_stop, e->stream))
+            return fail(e, STOMP_E_INVALID, "reuse: the source and destination rollout rows alias");
         return 0;
     }
     const size_t slot = (size_t)e->Kr * ((size_t)e->J * e->N + e->N);
@@ -837,7 +806,9 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         e->extra_added = true;
     }
     hipError_t st = hipGetLastError();
-    if (st != hipSuccess) return fail(e, STOMP_E_DEVICE, "kernel launch failed: %s", hipGetErrorString(st));
+    if (st != hipSuccess)
+        return fail(e, STOMP_E_DEVICE, "kernel launch failed: %s%s%s", hipGetErrorString(st),
+                    lds_opt_in_error()[0] ? "; " : "", lds_opt_in_error());
     return 0;
 }
 
@@ -1070,8 +1041,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (hipMemsetAsync(e->d_track, 0, sizeof(DevTrack), e->stream) != hipSuccess)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     if (hipMemsetAsync(e->d_cs, 1, 1, e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
-    CREATE_TRY(dev_alloc(e, &e->d_tmp_params, (size_t)std::max(e->Kr, 1) * J * N));
-    CREATE_TRY(dev_alloc(e, &e->d_tmp_state, (size_t)std::max(e->Kr, 1) * N));
     CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
     if (e->world > 1 && e->Kr > 0) {
         const size_t slot = (size_t)e->Kr * ((size_t)J * N + N);
@@ -1265,20 +1234,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
     m.QT = e->d_QT;
-    {
-        // the FK program's sphere runs in order: (frame slot, first sphere, end sphere)
-        std::vector<int> runs;
-        for (const FkOp& o : e->ops)
-            if (o.sph_end > o.sph_begin) runs.insert(runs.end(), {e->sphere_slot[o.sph_begin], o.sph_begin, o.sph_end, 0});
-        m.nruns = (int)runs.size() / 4;
-        int* d_runs;
-        if (runs.empty()) runs.assign(4, 0);
-        CREATE_TRY(upload(e, &d_runs, runs.data(), runs.size()));
-        m.runs = d_runs;
-        const char* sp = std::getenv("STOMP_SPLIT");
-        e->split = sp && sp[0] == '1' && N <= 256 && e->S > 0;
-        if (e->split) CREATE_TRY(ensure_split(e, e->K_loc + 1));
-    }
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
     int pad_cf = 0;
@@ -2199,7 +2154,7 @@ int stomp_group_create(stomp_engine* const* engines, int32_t n, stomp_group** ou
         if (e->J != e0->J || e->N != e0->N || e->K != e0->K || e->S != e0->S ||
             rollout_lds_bytes(e->model, e->model.pad_lds) != lds0)
             return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model)");
-        if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->pre_host != 1 || e->terms_on || e->split ||
+        if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->pre_host != 1 || e->terms_on ||
             e->split_modes || e->use_cum || e->J > 16)
             return gfail(nullptr, STOMP_E_UNSUPPORTED,
                          "groups run single-device engines without reuse, state-cost terms or cumulative costs");

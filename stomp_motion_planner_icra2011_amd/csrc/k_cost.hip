@@ -48,10 +48,6 @@ constexpr int rollout_min_waves()
 {
     return BLOCK == kBlock ? ROLLOUT_MIN_WAVES : (BLOCK > 512 ? 4 : 2);
 }
-#ifndef SPHERE_UNROLL
-#define SPHERE_UNROLL 2
-#endif
-constexpr int kSphereUnroll = SPHERE_UNROLL;   // spheres per pair lane with gathers in flight (GATHER_ROUNDS)
 // spheres of one run a pair lane takes: run_max(N) / (BLOCK / N) <= 16 / 2 (N <= 128) or 8 / 1
 constexpr int kLaneSpheres = 8;
 static_assert(kRunMaxSmall / 2 <= kLaneSpheres && kRunMaxLarge <= kLaneSpheres && kBlock >= 256,
@@ -214,8 +210,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     }
     STAMP(6);
     // phased with x in the a-value buffers: the control costs are made during the FK program
-    // (not for the split pipeline's preparation launch, which ends before the FK program)
-    const bool defer = PHASED && L.nzA == L.av && (gen || pre) && !a.prep_only;
+    const bool defer = PHASED && L.nzA == L.av && (gen || pre);
     if (gen) {
         if (defer) rollout_project<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
         else rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
@@ -294,9 +289,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
     if (tout)
         for (int idx = tid; idx < J * N; idx += BLOCK) tout[idx] = traj[idx];
-    // split pipeline: the joint-limited trajectory is all this launch makes; k_fk, k_pairs and
-    // k_fold (k_split.hip) evaluate it
-    if (a.prep_only) return;
     __syncthreads();
     STAMP(3);
 
@@ -304,11 +296,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     // FK / fold lane: waypoint t_own (< N).  Odd workgroups run the FK program on waves 2-3
     // (N <= 128): two workgroups share a CU, and their waves 0-1 would otherwise share SIMDs
     // while the FK-idle waves leave the other two SIMDs empty
-#ifndef FK_NO_SPREAD
     const int t_own = tid - ((N <= 128 && (e & 1)) ? 128 : 0);
-#else
-    const int t_own = tid;
-#endif
     const bool fk_lane = t_own >= 0 && t_own < N;
     const int G = BLOCK / N, pg = tid / N, pt = tid - pg * N;   // pair lanes: (group, waypoint)
     // C: running frame in the registers of lanes t < N; branch-point frames saved in LDS
@@ -523,10 +511,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // re-publish the same frame
         const int sb = o.sph_begin, se = o.sph_end;
         const int ns = se - sb;
-        int next = -1;
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
-        // flight) and serves spheres g, g + G, ... of the slot, kSphereUnroll gathers in flight
-#ifndef GATHER_ROUNDS
+        // flight) and serves spheres g, g + G, ... of the slot
         if (pg < G) {
             // every sphere of the run this lane takes (at most kLaneSpheres: a run holds <= 16
             // spheres and G >= 2 when N <= 128; <= 8 spheres and G >= 1 otherwise) is looked up
@@ -571,57 +557,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 }
             }
         }
-#else
-        if (pg < G) {
-            double F[12];
-#pragma unroll
-            for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
-            for (int q0 = pg; q0 < ns; q0 += G * kSphereUnroll) {
-                float dv[kSphereUnroll];
-#pragma unroll
-                for (int u = 0; u < kSphereUnroll; ++u) {
-                    const double* pos = sph[sb + min(q0 + u * G, ns - 1)].pos;
-                    double x[3];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i)
-                        x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
-                    dv[u] = sdf_distance(m, x);
-                }
-                STAMP(40 + run);
-#ifdef FK_PIPELINE
-                // while the first gathers are in flight, lanes t < N run the FK program on to
-                // the next slot's frame (C; the published frame stays in fb for this slot).
-                // Off by default: at the 168-VGPR cap the frame spills, and the spill reloads
-                // wait on the gathers (one vmcnt counter)
-                if (next < 0) next = fk_advance(op + 1);
-#endif
-#pragma unroll
-                for (int u = 0; u < kSphereUnroll; ++u) {
-                    const int q = q0 + u * G;
-                    const bool in = q < ns;
-                    double pot = 0.0;
-                    if (in) {
-                        const DevSphere& sp = sph[sb + q];
-                        const double dd = (double)dv[u];
-                        col |= dd <= sp.radius;
-                        pot = potential(sp, dd);
-                        av[q * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
-                    }
-                    // append (q, t) with pot != 0 to the slot's list: one LDS atomic per wave
-                    const bool nz = in && pot != 0.0;
-                    const unsigned long long mask = __ballot(nz);
-                    if (mask) {
-                        const int lane_id = tid & 63;
-                        const int leader = __ffsll((long long)mask) - 1;
-                        int base = 0;
-                        if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                        base = __shfl(base, leader, 64);
-                        if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
-                    }
-                }
-            }
-        }
-#endif
         __syncthreads();   // pots and the non-zero list complete
         STAMP(11 + 4 * run);
         // velocities only for the listed pairs, spread densely over the block: usually fewer
@@ -632,7 +567,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             const int qi = it / N, ti = it - qi * N;
             av[it] *= sphere_speed(m, fb, pad, sph[sb + qi], sb + qi, ti);
         }
-#ifndef FK_PIPELINE
         // C is reloaded from fb (not kept live across the pairs)
         if (fk_lane) {
 #pragma unroll
@@ -640,7 +574,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
             for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
         }
-#endif
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
         __builtin_amdgcn_s_setprio(3);
@@ -659,10 +592,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 }
             }
         }
-        // lanes that ran no pair round (or the unpipelined build) advance here; the
-        // program's control flow is uniform, so every lane arrives at the same next op
-        if (next < 0) next = fk_advance(op + 1);
-        op = next;
+        // the program's control flow is uniform, so every lane arrives at the same next op
+        op = fk_advance(op + 1);
         __builtin_amdgcn_s_setprio(2);
         STAMP(13 + 4 * run);
         ++run;
@@ -851,260 +782,6 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     }
     if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock>, lds);
     hipLaunchKernelGGL((k_rollout<kBlock>), dim3(blocks), dim3(kBlock), lds, s, m, a);
-}
-
-// ===================================================================== split evaluation
-// The same Task::execute, cut along its phases so that every phase runs with all rollouts'
-// parallelism instead of as one workgroup's sequential chain (k_rollout alone is bound by
-// that chain: one rollout per CU runs as long as two):
-//   k_rollout (prep_only)  noise phase + handleJointLimits -> joint-limited trajectory rows
-//   k_fk                   one lane per (rollout, waypoint): the FK program, each
-//                          sphere-carrying segment's frame to HBM [rows][nslots][12][N]
-//   k_pairs                one workgroup per (rollout, sphere run): positions, SDF gathers,
-//                          potentials, velocities where the potential is non-zero; a = pot |v|
-//                          to HBM [rows][S][N] and the run's collision flag
-//   k_fold                 one lane per (rollout, waypoint): cum / state over the spheres in
-//                          list order (stomp_optimizer.cpp:1096-1105), costs, flag and total
-// Every value is computed by the same expression in the same order as k_rollout and the
-// oracle, so the results are bit-identical.
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fk(DevModel m, CostArgs a, SplitBufs b)
-{
-    // the program's tables in LDS and every (sin, cos) of the lane's waypoint computed up front
-    // (independent, all loads in flight), so the frame chain itself waits only on LDS reads
-    __shared__ DevSegment seg_s[kMaxSeg];
-    __shared__ FkOp ops_s[kMaxOps];
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    if (a.stop && *a.stop) return;
-    const int N = m.N, J = m.J;
-    const int e = blockIdx.x, t = threadIdx.x;
-    for (int i = t; i < m.nseg; i += BLOCK) seg_s[i] = m.segs[i];
-    for (int i = t; i < m.nops; i += BLOCK) ops_s[i] = m.ops[i];
-    const bool extra = e == a.num_noisy;
-    const double* traj = extra ? a.x_traj : a.traj_out + (long long)e * J * N;
-    double* sn = (double*)lds_raw;            // [J][BLOCK]
-    double* cs = sn + (size_t)J * BLOCK;      // [J][BLOCK]
-    if (t < N) {
-        for (int j0 = 0; j0 < J; j0 += 8) {
-            double q[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) q[u] = traj[min(j0 + u, J - 1) * N + t];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (j0 + u >= J) break;
-                double st, ct;
-                det_sincos(q[u], &st, &ct);
-                sn[(j0 + u) * BLOCK + t] = st;
-                cs[(j0 + u) * BLOCK + t] = ct;
-            }
-        }
-    }
-    __syncthreads();
-    if (t >= N) return;
-    double* fr = b.frames + (size_t)e * m.nslots * 12 * N;
-    Frame C, S0, S1;
-    for (int op = 0; op < m.nops; ++op) {
-        const FkOp o = ops_s[op];
-        if (o.seg < 0) continue;
-        const DevSegment& sg = seg_s[o.seg];
-        double st = 0.0, ct = 1.0;
-        if (sg.q_index >= 0) {
-            st = sn[sg.q_index * BLOCK + t];
-            ct = cs[sg.q_index * BLOCK + t];
-        }
-        fk_op(sg, o.base, o.save, st, ct, C, S0, S1);
-        if (o.slot >= 0) {
-            double* dst = fr + (size_t)o.slot * 12 * N + t;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) dst[k * N] = C.R[k];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
-        }
-    }
-}
-
-size_t split_pairs_lds_bytes(const DevModel& m)
-{
-    return align16((size_t)12 * m.N * sizeof(double)) + align16((size_t)m.sph_chunk * m.N * sizeof(double)) +
-           align16((size_t)m.sph_chunk * m.N * sizeof(unsigned short));
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_pairs(DevModel m, CostArgs a, SplitBufs b, int rows)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    __shared__ int nz_count;
-    const int N = m.N, S = m.S;
-    const int npair = m.nruns * rows;
-    if ((int)blockIdx.x >= npair) {
-        // the next iteration's pregen rows, at the default priority below the pair workgroups
-        // (as in k_rollout: no stop check, the rows stay valid for pre_it)
-        const NoiseArgs& pa = a.pre_next;
-        const RolloutLds L = rollout_lds(pa.J, pa.N, 0, 0, 0, 0, 0, 0, 0);
-        double* pA = (double*)lds_raw;
-        double* pB = (double*)(lds_raw + (L.nzB - L.nzA));
-        const int r = blockIdx.x - npair;
-        rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
-        if (pa.J <= 8) {
-            pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
-            pregen_meps_ng<BLOCK, 2>(pa, r, pB, threadIdx.x);
-        } else {
-            pregen_eps_ng<BLOCK, 4>(pa, r, pA, pB, threadIdx.x);
-            pregen_meps_ng<BLOCK, 4>(pa, r, pB, threadIdx.x);
-        }
-        return;
-    }
-    if (a.pre_rows > 0) __builtin_amdgcn_s_setprio(2);
-    if (a.stop && *a.stop) return;
-    const int e = blockIdx.x / m.nruns, run = blockIdx.x - e * m.nruns, tid = threadIdx.x;
-    const int slot = m.runs[4 * run], sb = m.runs[4 * run + 1], se = m.runs[4 * run + 2];
-    const int ns = se - sb;
-    double* fb = (double*)lds_raw;
-    double* av = (double*)(lds_raw + align16((size_t)12 * N * sizeof(double)));
-    unsigned short* nzl = (unsigned short*)((unsigned char*)av + align16((size_t)m.sph_chunk * N * sizeof(double)));
-    const double* fr = b.frames + ((size_t)e * m.nslots + slot) * 12 * N;
-    for (int i = tid; i < 12 * N; i += BLOCK) fb[i] = fr[i];
-    if (tid == 0) nz_count = 0;
-    __syncthreads();
-    const int G = BLOCK / N, pg = tid / N, pt = tid - pg * N;
-    bool col = false;
-    if (pg < G) {
-        double F[12];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
-        constexpr int U = kLaneSpheres;
-        float dv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (u * G >= ns) break;   // uniform
-            const double* pos = m.sph[sb + min(pg + u * G, ns - 1)].pos;
-            double x[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
-            dv[u] = sdf_distance(m, x);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (u * G >= ns) break;   // uniform
-            const int q = pg + u * G;
-            const bool in = q < ns;
-            double pot = 0.0;
-            if (in) {
-                const DevSphere& sp = m.sph[sb + q];
-                const double dd = (double)dv[u];
-                col |= dd <= sp.radius;
-                pot = potential(sp, dd);
-                av[q * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
-            }
-            const bool nz = in && pot != 0.0;
-            const unsigned long long mask = __ballot(nz);
-            if (mask) {
-                const int lane_id = tid & 63;
-                const int leader = __ffsll((long long)mask) - 1;
-                int base = 0;
-                if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                base = __shfl(base, leader, 64);
-                if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
-            }
-        }
-    }
-    const int any_col = __syncthreads_or(col ? 1 : 0);   // pots and the non-zero list complete
-    for (int i = tid; i < nz_count; i += BLOCK) {
-        const int it = nzl[i];
-        const int qi = it / N, ti = it - qi * N;
-        av[it] *= sphere_speed(m, fb, m.pad_pos, m.sph[sb + qi], sb + qi, ti);
-    }
-    __syncthreads();
-    double* out = b.aval + ((size_t)e * S + sb) * N;
-    for (int i = tid; i < ns * N; i += BLOCK) out[i] = av[i];
-    if (tid == 0) b.colf[e * m.nruns + run] = any_col;
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fold(DevModel m, CostArgs a, SplitBufs b)
-{
-    __shared__ double cst[256];
-    if (a.stop && *a.stop) return;
-    const int N = m.N, S = m.S;
-    const int e = blockIdx.x, t = threadIdx.x;
-    const bool extra = e == a.num_noisy;
-    const int member = extra ? a.x_member : a.member;
-    if (t < N) {
-        const double* av = b.aval + (size_t)e * S * N + t;
-        double cum = 0.0, state = 0.0;
-        // batches of 32 loads, the next batch in flight while this one is summed sequentially
-        constexpr int FB = 32;
-        double v0[FB], v1[FB];
-        auto load = [&](double* v, int q0) {
-#pragma unroll
-            for (int q = 0; q < FB; ++q) v[q] = av[(size_t)min(q0 + q, S - 1) * N];
-        };
-        auto fold = [&](const double* v, int q0) {
-#pragma unroll
-            for (int q = 0; q < FB; ++q) {
-                if (q0 + q >= S) break;
-                cum += v[q];
-                state += cum;
-            }
-        };
-        load(v0, 0);
-        for (int q0 = 0; q0 < S; q0 += 2 * FB) {
-            if (q0 + FB < S) load(v1, q0 + FB);
-            fold(v0, q0);
-            if (q0 + FB >= S) break;
-            if (q0 + 2 * FB < S) load(v0, q0 + 2 * FB);
-            fold(v1, q0 + FB);
-        }
-        const double cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
-        double* so = extra ? a.x_state : a.state_out + (long long)e * N;
-        so[t] = cost;
-        cst[t] = cost;
-    }
-    __syncthreads();
-    if (t == 0) {
-        int flag = 0;
-        for (int r = 0; r < m.nruns; ++r) flag |= b.colf[e * m.nruns + r];
-        const bool cf = !flag && !(member == 0 && m.pad_collision);
-        uint8_t* cfo = extra ? a.x_cf : (a.cf_out ? a.cf_out + e : nullptr);
-        double* to = extra ? a.x_total : (a.total_out ? a.total_out + e : nullptr);
-        if (cfo) *cfo = cf ? 1 : 0;
-        if (to) {
-            double s = 0.0;   // costs.sum() (:1155), sequential
-            for (int k = 0; k < N; ++k) s += cst[k];
-            *to = s;
-        }
-    }
-}
-
-void launch_split_eval(const DevModel& m, const CostArgs& a, const SplitBufs& b, hipStream_t s)
-{
-    const int rows = a.num_noisy + (a.x_params ? 1 : 0);
-    CostArgs prep = a;
-    prep.prep_only = 1;
-    prep.pre_rows = 0;         // the pregen rows ride in the k_pairs launch
-    launch_cost(m, prep, s);   // noise phase, joint limits, trajectory rows
-    if (rows <= 0 && a.pre_rows <= 0) return;
-    const int lanes = m.N <= 64 ? 64 : (m.N <= 128 ? 128 : 256);
-    if (rows > 0) {
-        const size_t fk_lds = (size_t)2 * m.J * lanes * sizeof(double);
-        if (lanes == 64) hipLaunchKernelGGL((k_fk<64>), dim3(rows), dim3(64), fk_lds, s, m, a, b);
-        else if (lanes == 128) hipLaunchKernelGGL((k_fk<128>), dim3(rows), dim3(128), fk_lds, s, m, a, b);
-        else hipLaunchKernelGGL((k_fk<256>), dim3(rows), dim3(256), fk_lds, s, m, a, b);
-    }
-    size_t lds = split_pairs_lds_bytes(m);
-    const int pre = a.pre_rows > 0 ? a.pre_rows : 0;
-    if (pre) {
-        const RolloutLds L = rollout_lds(a.pre_next.J, a.pre_next.N, 0, 0, 0, 0, 0, 0, 0);
-        lds = std::max(lds, (size_t)2 * (L.nzB - L.nzA));
-    }
-    if (lds > 64 * 1024) lds_opt_in((const void*)k_pairs<256>, lds);
-    hipLaunchKernelGGL((k_pairs<256>), dim3(m.nruns * rows + pre), dim3(256), lds, s, m, a, b, rows);
-    if (rows <= 0) return;
-    if (lanes == 64) hipLaunchKernelGGL((k_fold<64>), dim3(rows), dim3(64), 0, s, m, a, b);
-    else if (lanes == 128) hipLaunchKernelGGL((k_fold<128>), dim3(rows), dim3(128), 0, s, m, a, b);
-    else hipLaunchKernelGGL((k_fold<256>), dim3(rows), dim3(256), 0, s, m, a, b);
 }
 
 }  // namespace stomp

@@ -6,11 +6,16 @@
 
 #include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 
 namespace stomp {
 
-void lds_opt_in(const void* kernel, size_t bytes)
+namespace {
+thread_local std::string g_opt_in_error;   // the last failed opt-in on this host thread
+}
+
+hipError_t lds_opt_in(const void* kernel, size_t bytes)
 {
     static std::mutex mu;
     static std::map<std::pair<const void*, int>, size_t> raised;
@@ -18,10 +23,22 @@ void lds_opt_in(const void* kernel, size_t bytes)
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lock(mu);
     size_t& r = raised[{kernel, dev}];
-    if (bytes > r) {
-        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        r = bytes;
+    if (bytes <= r) return hipSuccess;
+    const hipError_t st = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (st != hipSuccess) {
+        // not recorded as raised: the next launch retries, and the launch error names the size
+        g_opt_in_error = "dynamic LDS opt-in of " + std::to_string(bytes) + " bytes on device " + std::to_string(dev) +
+                         " failed: " + hipGetErrorString(st);
+        (void)hipGetLastError();
+        return st;
     }
+    r = bytes;
+    return hipSuccess;
+}
+
+const char* lds_opt_in_error()
+{
+    return g_opt_in_error.c_str();
 }
 
 // padding-point sphere positions: iteration-0 full FK of start (rows 0..5) and goal (rows 6..11)
@@ -142,8 +159,7 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
                                                const double* src_params, const double* src_state,
                                                const double* control, double* params, double* noise, double* state,
                                                const double* x_params, const double* x_state,
-                                               const double* x_control, const double* theta, double* tmp_params,
-                                               double* tmp_state, const int* stop)
+                                               const double* x_control, const double* theta, const int* stop)
 {
     if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
@@ -166,10 +182,8 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
         if (rank < Kr) sel[rank] = c;
     }
     __syncthreads();
-    // the kept rows into rows K_gen.. of this iteration's set (the engine's row sets are distinct
-    // buffers, so the reads need no staging copy): four independent loads in flight per lane
-    (void)tmp_params;
-    (void)tmp_state;
+    // the kept rows into rows K_gen.. of this iteration's set (the row sets are distinct buffers,
+    // launch_reuse checks it, so the reads need no staging copy)
     const double* __restrict__ sp = src_params;
     const double* __restrict__ ss = src_state;
     // row by row (no per-element 64-bit division), four independent loads in flight per lane
@@ -201,16 +215,19 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
     }
 }
 
-void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
-                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
-                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                  double* tmp_params, double* tmp_state, const int* stop, hipStream_t s)
+int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
+                 const double* src_state, const double* src_control, double* params, double* noise, double* state,
+                 const double* x_params, const double* x_state, const double* x_control, const double* theta,
+                 const int* stop, hipStream_t s)
 {
+    // k_reuse copies straight from the source rows into rows K_gen..: an in-place call would read
+    // rows this same loop already overwrote
+    if (src_params == params || src_state == state) return -1;
     const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
     if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);   // K in the thousands
     hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
-                       src_control, params, noise, state, x_params, x_state, x_control, theta, tmp_params, tmp_state,
-                       stop);
+                       src_control, params, noise, state, x_params, x_state, x_control, theta, stop);
+    return 0;
 }
 
 // ---- the same reuse step with the K rows sharded over ranks: every rank prices its

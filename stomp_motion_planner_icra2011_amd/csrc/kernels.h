@@ -86,8 +86,6 @@ struct DevModel {
     double w_obs, w_con, w_tq;
     int pad_collision;
     const double* QT;           // [J][N][N]
-    int nruns;                  // sphere runs of the FK program (ops with spheres), in sphere order
-    const int* runs;            // [nruns][4]: frame slot, first sphere, end sphere, 0
 };
 
 
@@ -183,7 +181,6 @@ struct CostArgs {
     double* total_out;          // [num_noisy] or null
     const double* x_params;     // [J][N] or null
     int x_member;
-    int prep_only;              // 1: noise phase + handleJointLimits + traj_out / x_traj only (split pipeline)
     int pre_rows;               // > 0: blocks after the rollouts make k_pregen's rows of pre_next (the
     NoiseArgs pre_next;         // next iteration) at low priority in the same dispatch
     double* x_state;
@@ -197,16 +194,6 @@ struct CostArgs {
     double* x_prm;
     double* x_nse;
 };
-
-// Buffers of the split evaluation pipeline (k_rollout prep_only -> k_fk -> k_pairs -> k_fold),
-// rows = the launch's noisy rollouts and the noiseless one (row num_noisy)
-struct SplitBufs {
-    double* frames;             // [rows][nslots][12][N] FK frame of every sphere-carrying segment
-    double* aval;               // [rows][S][N] a = pot * |v| (stomp_optimizer.cpp:1100-1105)
-    int* colf;                  // [rows][nruns] any sphere of the run in collision
-};
-void launch_split_eval(const DevModel& m, const CostArgs& a, const SplitBufs& b, hipStream_t s);
-size_t split_pairs_lds_bytes(const DevModel& m);
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
 
@@ -275,9 +262,11 @@ struct TermsArgs {
 };
 
 // hipFuncAttributeMaxDynamicSharedMemorySize opt-in for more than the default dynamic LDS:
-// remembered per (kernel, current device), thread-safe (engines on several devices or host
-// threads share the kernels)
-void lds_opt_in(const void* kernel, size_t bytes);
+// remembered per (kernel, current device) once it succeeds, thread-safe (engines on several
+// devices or host threads share the kernels).  A failure is left for the launch to report, with
+// the message of lds_opt_in_error() (this host thread's last failed opt-in, or "").
+hipError_t lds_opt_in(const void* kernel, size_t bytes);
+const char* lds_opt_in_error();
 
 size_t terms_lds_bytes(const TermsModel& m);
 void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
@@ -340,11 +329,12 @@ void launch_gather_max(const double* gathered, int world, int n, double* out, hi
 void launch_pad_fk(const DevModel& m, const double* start, const double* goal, double* pad_pos, int* pad_cf,
                    hipStream_t s);
 // src_*: the previous iteration's rows (ranked, copied from); params / noise / state: this
-// iteration's rows K_gen.. (written); the two may be the same buffers
-void launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
-                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
-                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                  double* tmp_params, double* tmp_state, const int* stop, hipStream_t s);
+// iteration's rows K_gen.. (written).  The two row sets must be distinct buffers (the copy has no
+// staging pass); returns -1 without launching when they alias.
+int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
+                 const double* src_state, const double* src_control, double* params, double* noise, double* state,
+                 const double* x_params, const double* x_state, const double* x_control, const double* theta,
+                 const int* stop, hipStream_t s);
 // sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
 // noise = eps, params = theta_gen + eps of rows left in a pregen buffer (rows_in_pre)
 void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,

@@ -384,25 +384,3 @@ def test_optimize_statistics_torques_and_durations():
         assert est.collision_success_duration <= est.success_duration < 30.0
     else:
         assert est.success_duration == 0.0
-
-
-@pytest.mark.parametrize("K,Kr,waypoints,dof", [(64, 0, 100, 7), (20, 10, 100, 7), (16, 0, 200, 14)])
-def test_split_pipeline_bitwise(monkeypatch, K, Kr, waypoints, dof):
-    # STOMP_SPLIT=1: Task::execute as k_rollout (prep) -> k_fk -> k_pairs -> k_fold
-    monkeypatch.setenv("STOMP_SPLIT", "1")
-    p = make(K=K, Kr=Kr, waypoints=waypoints, dof=dof)
-    o, e = po.Oracle(p, threads=8), eng.Engine(p)
-    for it in range(1, 5):
-        _compare_iteration(o, e, it)
-    e.run(5, 4)
-    for it in range(5, 9):
-        o.iterate(it)
-    np.testing.assert_array_equal(e.theta(), o.theta())
-    np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory())
-    params = o.rollouts("params")[:3]
-    c, cf, tr = e.execute(params, iteration_member=0)
-    for r in range(3):
-        oc, ocf, otr = o.execute(params[r], iteration_member=0)
-        np.testing.assert_array_equal(c[r], oc)
-        np.testing.assert_array_equal(tr[r], otr)
-        assert bool(cf[r]) == ocf
