@@ -1,0 +1,88 @@
+"""the CPU oracle and the host-side facade built with
+-fsanitize=address,undefined and run in the container (no GPU).
+
+* oracle/oracle_driver.c (optimize, more iterations, per-rollout execute) under ASan + UBSan
+  must finish cleanly and print exactly what the uninstrumented oracle (oracle/pyoracle.py)
+  computes on the same problem.
+* tests/facade_driver.cpp + facade/stomp_facade.cpp (the reference-shaped C++ classes) under
+  ASan + UBSan, in the driver's device-free `validate` mode (argument checks of StompOptimizer,
+  PolicyImprovement and PolicyImprovementLoop).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from stomp_motion_planner_icra2011_amd import problem as pb
+from tests import facade_util as fu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN_ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+def _oracle_driver():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "sanitize"])
+    return os.path.join(ROOT, "build", "san", "oracle_driver_san")
+
+
+def _expected(p):
+    o = po.Oracle(p, threads=1)
+    st, costs = o.optimize()
+    lines = [f"{st.iterations} {st.success_iteration} {st.collision_success_iteration}"]
+    lines += [repr(float(c)) for c in costs]
+    lines += [repr(float(v)) for v in o.best_trajectory().ravel()]
+    for it in range(st.iterations + 1, st.iterations + 4):
+        c, cf = o.iterate(it)
+        lines.append(f"{c!r} {int(cf)}")
+    lines += [repr(float(v)) for v in o.theta().ravel()]
+    params = o.rollouts("params")
+    for r in range(min(p.params.num_rollouts, 4)):
+        c, cf, tr = o.execute(params[r], iteration_member=1)
+        lines += [repr(float(v)) for v in c]
+        lines += [repr(float(v)) for v in tr.ravel()]
+        lines.append(str(int(cf)))
+    return lines
+
+
+@pytest.mark.parametrize("K,Kr,dof,waypoints", [(20, 10, 7, 100), (12, 0, 14, 100)])
+def test_oracle_under_asan_ubsan(tmp_path, K, Kr, dof, waypoints):
+    exe = _oracle_driver()
+    p = pb.make_problem(dof=dof, waypoints=waypoints, grid_n=32, num_rollouts=K, num_reused_rollouts=Kr,
+                        max_iterations=12)
+    prob, sdf = fu.write_problem(p, str(tmp_path))
+    out = str(tmp_path / "out.txt")
+    r = subprocess.run([exe, prob, sdf, out, "1"], capture_output=True, text=True, timeout=600, env=SAN_ENV)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    got = open(out).read().split("\n")[:-1]
+    want = _expected(p)
+    assert len(got) == len(want)
+    # %.17g (C) and repr (Python) print the same double differently; compare the values
+    for g, w in zip(got, want):
+        gv, wv = g.split(), w.split()
+        assert len(gv) == len(wv)
+        for a, b in zip(gv, wv):
+            assert np.float64(a) == np.float64(b) or (np.isnan(float(a)) and np.isnan(float(b))), (g, w)
+
+
+def test_facade_under_asan_ubsan(tmp_path):
+    from stomp_motion_planner_icra2011_amd import _build
+    lib = _build.build()
+    exe = str(tmp_path / "facade_driver_san")
+    subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-Wall", "-fno-omit-frame-pointer",
+                           "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                           "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "facade_driver.cpp"),
+                           os.path.join(ROOT, "stomp_motion_planner_icra2011_amd", "facade", "stomp_facade.cpp"),
+                           "-o", exe, lib, "-Wl,-rpath," + os.path.dirname(lib)])
+    p = pb.make_problem(grid_n=16, num_rollouts=10, num_reused_rollouts=5)
+    prob, sdf = fu.write_problem(p, str(tmp_path))
+    # the HIP runtime's own allocations are not ours to leak-check
+    env = dict(SAN_ENV, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1")
+    r = subprocess.run([exe, prob, sdf, "validate"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "validate OK" in r.stdout
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
