@@ -22,10 +22,14 @@ Also reported:
                 rollouts and the deferred noiseless one): achieved = SURVEY.md 8(d) algorithmic
                 bytes per unit (4 S + 16 J + 8) x (K_loc + 1) N units / its HIP-event average
                 duration (second pass of the same K steps with events; the value pass has none);
-                traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
+                traffic = HBM bytes per launch from the committed rocprofv3 PMC summary of
+                this very build (matched by the engine's source hash; null otherwise);
+  valu          the same kernel's VALU issue fraction: SQ_INSTS_VALU (that PMC summary) x 4
+                cycles / 1024 SIMDs / (the event-measured duration x 2.4 GHz)
   cpu_baseline  the CPU oracle (oracle/, reference-structure dense products, 1 thread) timed on
                 this host on a bounded sample of the same workload; cpu_baseline_all_cores the
-                banded oracle over the host cores this process may use
+                banded oracle over the CPU share this job is granted (the cgroup quota when one is
+                set, else OMP_NUM_THREADS, else the affinity mask), all three counts reported
 """
 from __future__ import annotations
 
@@ -42,6 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_CLOCK_HZ = 2.4e9  # MI355X peak engine clock; 256 CUs x 4 SIMDs, a wave64 VALU op issues in 4 cycles
 METRIC = "STOMP iterations/sec (7-DOF, 100 wp, K=512, 256³ SDF) at 1/2/4/8 GPUs"
 
 # BASELINE.json configs[0..4] (configs[0], cfg1, is the reference's own CPU case: K = 20 with
@@ -88,18 +93,45 @@ def workload_name(args) -> str:
     return args.workload + (" (modified)" if args.custom else "")
 
 
-def latest_traffic():
-    """HBM bytes per k_rollout launch from the newest committed rocprofv3 PMC summary (cfg2, one
-    GPU), FETCH_SIZE with and without the gfx950 x2 correction."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*rollout_cost_traffic*.json")))
-    if not files:
-        return None, None, None
+def pmc_summary():
+    """The newest committed rocprofv3 PMC summary (tools/pmc_traffic.py) of the default workload
+    and whether it was taken of this build (the engine's source hash).  Returns (summary or None,
+    provenance dict)."""
+    from stomp_motion_planner_icra2011_amd import _build
+    here = _build.source_hash()
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*rollout_cost_traffic*.json")), key=os.path.getmtime)
+    newest = None
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if newest is None:
+            newest = (os.path.basename(path), d.get("source_hash"))
+        if d.get("source_hash") == here:
+            return d, {"file": os.path.basename(path), "source_hash": here, "matches_build": True}
+    return None, {"file": newest[0] if newest else None, "source_hash": newest[1] if newest else None,
+                  "build_source_hash": here, "matches_build": False,
+                  "note": "no PMC pass of this build is committed: traffic and VALU counts are null"}
+
+
+def cpu_share():
+    """CPUs this job may use: the cgroup quota (v2 cpu.max or v1 cfs quota) when one is set."""
+    quota = None
     try:
-        with open(files[-1]) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d.get("hbm_bytes_per_launch_uncorrected"), os.path.basename(files[-1])
-    except Exception:
-        return None, None, None
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    return quota
 
 
 def host_info():
@@ -115,8 +147,8 @@ def host_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    return {"nproc": os.cpu_count(), "sched_affinity": avail, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "model": model}
+    return {"nproc": os.cpu_count(), "sched_affinity": avail, "cgroup_cpu_quota": cpu_share(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
 
 
 def cpu_baseline(problem, budget_s: float):
@@ -140,9 +172,19 @@ def cpu_baseline(problem, budget_s: float):
 
 def cpu_baseline_all_cores(problem, budget_s: float):
     """SURVEY.md 8(d)'s stronger CPU baseline: the oracle with banded stencils and Task::execute
-    spread over the host cores this process may use (OpenMP over rollouts)."""
+    spread over the host cores this job is granted (OpenMP over rollouts).  The GPU box's
+    affinity mask shows the whole machine, but a one-GPU job's CPU share is a fraction of it
+    (the harness sets OMP_NUM_THREADS to it); threads past the share only time-slice."""
     from oracle import pyoracle as po
-    threads = int(os.environ.get("OMP_NUM_THREADS") or host_info()["sched_affinity"] or 1)
+    h = host_info()
+    quota = h["cgroup_cpu_quota"]
+    if quota:
+        threads, basis = max(1, int(quota)), "cgroup CPU quota"
+    elif os.environ.get("OMP_NUM_THREADS"):
+        threads, basis = int(os.environ["OMP_NUM_THREADS"]), "OMP_NUM_THREADS (the job's CPU share)"
+    else:
+        threads, basis = int(h["sched_affinity"] or 1), "affinity mask"
+    threads = min(threads, int(h["sched_affinity"] or threads))
     o = po.Oracle(problem, dense=False, threads=threads)
     t0 = time.perf_counter()
     n = 0
@@ -152,9 +194,11 @@ def cpu_baseline_all_cores(problem, budget_s: float):
         el = time.perf_counter() - t0
         if el >= budget_s or n >= 400:
             break
-    return {"value": n / el, "unit": "iterations/s", "cores": threads, "kind": "port", "host": host_info(),
+    return {"value": n / el, "unit": "iterations/s", "cores": threads, "cores_basis": basis,
+            "affinity_cores": h["sched_affinity"], "kind": "port", "host": h,
             "sample": f"first {n} iterations of the same workload on the CPU oracle with banded stencils and "
-                      f"OpenMP over the rollouts' Task::execute, {threads} threads, {el:.1f} s"}
+                      f"OpenMP over the rollouts' Task::execute, {threads} threads ({basis}; affinity mask "
+                      f"{h['sched_affinity']} CPUs), {el:.1f} s"}
 
 
 def max_over_ranks(dist, x: float) -> float:
@@ -351,14 +395,13 @@ def main():
     if timing.get("rollout_cost", {}).get("launches"):
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
         achieved = bytes_per_launch / avg_s / 1e9
-        traffic, traffic_raw, traffic_src = latest_traffic()
         headline = args.workload == "cfg2" and not args.custom and world == 1
+        pmc, prov = pmc_summary() if headline else (None, {"note": "PMC summaries are of cfg2 on one GPU"})
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    # the committed PMC summary is of the default workload (cfg2, one GPU)
-                    "traffic": traffic if headline else None,
-                    "traffic_uncorrected": traffic_raw if headline else None,
-                    "traffic_source": traffic_src if headline else None,
+                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                    "traffic_uncorrected": pmc.get("hbm_bytes_per_launch_uncorrected") if pmc else None,
+                    "traffic_source": prov,
                     "kernel": "k_rollout", "unit_bytes": unit_bytes, "units_per_launch": rows_launch * p.N,
                     "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3),
                     "frac_vs_measured_6290": round(achieved / 6290.0, 5),
@@ -367,6 +410,13 @@ def main():
                     "iteration_bytes": (K - args.reused + 1) * p.N * unit_bytes,
                     "iteration_frac": round((K - args.reused + 1) * p.N * unit_bytes * value /
                                             (HBM_PEAK_GBS * 1e9 * world), 5)}
+        # the bound that actually binds: fp64 VALU issue (SQ_INSTS_VALU of the same build's PMC pass)
+        insts = pmc.get("valu_insts_per_launch") if pmc else None
+        roofline["valu"] = {
+            "insts_per_launch": insts,
+            "issue_cycles_per_simd": round(insts * 4.0 / 1024, 1) if insts else None,
+            "frac_valu_issue": round(insts * 4.0 / 1024 / (avg_s * VALU_CLOCK_HZ), 4) if insts else None,
+            "clock_ghz": VALU_CLOCK_HZ / 1e9, "simds": 1024, "source": prov}
 
     # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
     # the same iterations with the optimizer's bookkeeping, no early stop

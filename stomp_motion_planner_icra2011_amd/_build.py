@@ -26,6 +26,18 @@ COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "
 ARCH = ["--offload-arch=gfx950"]
 
 
+def source_hash() -> str:
+    """sha256 (16 hex digits) of the engine library's sources: identifies the build a profile was
+    taken of (tools/pmc_traffic.py records it; bench.py reports PMC numbers only for a match)."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "stomp_engine.h")]:
+        with open(path, "rb") as f:
+            h.update(os.path.basename(path).encode() + b"\0" + f.read())
+    h.update(" ".join(f for f in COMMON + ARCH if not f.startswith("-I")).encode())   # no checkout paths
+    return h.hexdigest()[:16]
+
+
 def _newer(target: str, deps) -> bool:
     if not os.path.exists(target):
         return True

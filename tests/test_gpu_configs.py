@@ -6,11 +6,14 @@ bound on best_group_trajectory_ for the optimize runs:
 
   cfg2  7-DOF, N=99, K=512, 256^3 device-built SDF: 10 iterations, every rollout field,
         then StompOptimizer::optimize for 100 iterations
-  cfg3  7-DOF, N=199, 256^3: the per-GPU shard shape K=512, and the whole K=4096
-        iteration on one device (plain and through the sharded weights phases)
-  cfg4  14-DOF, N=99, K=1024, 512^3 device-built SDF (the HBM-bound field)
-  cfg5  8 planning problems (K=128 each, distinct start / goal / seed) on separate
-        engine streams sharing one device SDF, enqueued interleaved as bench.py does
+  cfg3  7-DOF, N=199, 256^3: the per-GPU shard shape K=512, the whole K=4096 iteration on one
+        device (plain and through the sharded weights phases), and StompOptimizer::optimize
+        over 25 iterations of the whole K=4096
+  cfg4  14-DOF, N=99, K=1024, 512^3 device-built SDF (the HBM-bound field): 3 iterations
+        field by field, then StompOptimizer::optimize over 25 iterations
+  cfg5  the bench's own shape: 64 planning problems (K=128 each, distinct start / goal / seed)
+        as ONE engine group (stomp_group_run, shared launches) on one device SDF; and 8
+        problems on separate engine streams, enqueued interleaved
 
 The distance field is built on the device by stomp_sdf_build (as bench.py does) and copied
 to the host for the oracle.  Reference: policy_improvement_loop.cpp:143-202.
@@ -150,8 +153,37 @@ def test_half_width_weights_tiles_bitwise(sdf256_n199, K, reused):
         compare_iteration(o, e, it)
 
 
+def optimize_matches(o, e, iterations):
+    """StompOptimizer::optimize (stomp_optimizer.cpp:249-401) on both sides: the same statistics,
+    the same per-iteration costs, and best_group_trajectory_ within the north-star 1e-5 and bit
+    for bit."""
+    ost, ocosts = o.optimize()
+    est, ecosts = e.optimize()
+    assert est.iterations == ost.iterations == iterations
+    assert (est.success, est.success_iteration, est.collision_success_iteration, est.last_improvement_iteration) == \
+        (ost.success, ost.success_iteration, ost.collision_success_iteration, ost.last_improvement_iteration)
+    np.testing.assert_array_equal(ecosts, ocosts)
+    eb, ob = e.best_trajectory(), o.best_trajectory()
+    assert np.max(np.abs(eb - ob)) <= TOL_FINAL
+    np.testing.assert_array_equal(eb, ob)
+    np.testing.assert_array_equal(e.theta(), o.theta())
+
+
+def test_cfg3_optimize_whole_K(sdf256_n199):
+    # cfg3's whole K = 4096 rollouts at N = 199 through the device-resident optimize loop
+    base, buf = sdf256_n199
+    p = pb.make_problem(dof=7, waypoints=200, grid_n=256, num_rollouts=4096, num_reused_rollouts=0,
+                        build_grid=False, max_iterations=25, max_iterations_after_collision_free=1000)
+    p.sdf = base.sdf
+    o = po.Oracle(p, threads=THREADS)
+    e = eng.Engine(p, sdf_device_ptr=buf.ptr)
+    optimize_matches(o, e, 25)
+    e.close()
+
+
 def test_cfg4_dual_arm_512_grid_bitwise():
-    p, buf = problem_on_device_sdf(dof=14, waypoints=100, grid_n=512, num_rollouts=1024, num_reused_rollouts=0)
+    p, buf = problem_on_device_sdf(dof=14, waypoints=100, grid_n=512, num_rollouts=1024, num_reused_rollouts=0,
+                                   max_iterations=25, max_iterations_after_collision_free=1000)
     try:
         assert p.J == 14 and len(p.spheres) > 90
         o = po.Oracle(p, threads=THREADS)
@@ -159,7 +191,53 @@ def test_cfg4_dual_arm_512_grid_bitwise():
         for it in range(1, 4):
             compare_iteration(o, e, it)
         e.close()
+        # the optimize loop from a fresh start, 25 iterations
+        o = po.Oracle(p, threads=THREADS)
+        e = eng.Engine(p, sdf_device_ptr=buf.ptr)
+        optimize_matches(o, e, 25)
+        e.close()
     finally:
+        buf.free()
+
+
+def test_cfg5_bench_shape_one_group():
+    # bench.py --workload cfg5 on one GPU: 64 problems (K = 128, 256^3), one engine group on one
+    # stream, the problems' offsets / seeds drawn as bench_problems draws them; two runs
+    base, buf = problem_on_device_sdf(dof=7, waypoints=100, grid_n=256, num_rollouts=128, num_reused_rollouts=0)
+    s = eng.Stream()
+    engines, oracles = [], []
+    try:
+        P = 64
+        rng = np.random.default_rng(1234)
+        offsets = rng.uniform(-0.15, 0.15, (P, 2, base.J))
+        for i in range(P):
+            d = offsets[i]
+            p = pb.make_problem(dof=7, waypoints=100, grid_n=256, num_rollouts=128, num_reused_rollouts=0,
+                                build_grid=False, seed=base.seed + 1 + i, start=list(base.start + d[0]),
+                                goal=list(base.goal + d[1]))
+            p.sdf = base.sdf
+            engines.append(eng.Engine(p, sdf_device_ptr=buf.ptr, stream=s.ptr))
+            oracles.append(po.Oracle(p, threads=THREADS))
+        group = eng.EngineGroup(engines)
+        for first, count in ((1, 5), (6, 4)):
+            group.run(first, count)
+            group.synchronize()
+            for o in oracles:
+                for it in range(first, first + count):
+                    o.iterate(it)
+            for i, (e, o) in enumerate(zip(engines, oracles)):
+                np.testing.assert_array_equal(e.theta(), o.theta(), err_msg=f"problem {i}")
+                np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory(), err_msg=f"problem {i}")
+                np.testing.assert_array_equal(e.rollouts("state_costs"), o.rollouts("state_costs"),
+                                              err_msg=f"problem {i}")
+                np.testing.assert_array_equal(e.rollouts("probabilities"), o.rollouts("probabilities"),
+                                              err_msg=f"problem {i}")
+        assert not np.array_equal(engines[0].theta(), engines[63].theta())
+        group.close()
+    finally:
+        for e in engines:
+            e.close()
+        s.close()
         buf.free()
 
 

@@ -7,7 +7,15 @@ dispatch from the L2's memory-side request counters (Infinity-Cache hits include
 on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled.  The
 rollout-cost stage is the fused k_rollout kernel (one launch per iteration).
 
-Usage: python tools/pmc_traffic.py <pmc dir> <out.json>
+SQ_INSTS_VALU (VALU instructions issued, summed over the launch's waves) gives the VALU issue
+fraction: SQ_INSTS_VALU x 4 cycles (a wave64 instruction on a 16-lane SIMD) / (CUs x 4 SIMDs) /
+(kernel duration x 2.4 GHz), with the duration from the kernel-trace stats of the same build
+(bench.py divides by its own event-measured duration).
+
+The summary records the engine's source hash (_build.source_hash): bench.py reports these
+numbers only while the sources are the ones profiled.
+
+Usage: python tools/pmc_traffic.py <pmc dir> <out.json> [kernel_stats.csv]
 """
 import csv
 import collections
@@ -21,11 +29,21 @@ def per_kernel(path):
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+    out = {}
+    for k, d in agg.items():
+        out[k] = {c: sum(v) / len(v) for c, v in d.items()}
+        out[k]["dispatches"] = max(len(v) for v in d.values())
+    return out
 
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from stomp_motion_planner_icra2011_amd import _build
+    durations = {}
+    if len(sys.argv) > 3:
+        for r in csv.DictReader(open(sys.argv[3])):
+            durations[r["Name"].split("(")[0].replace("void ", "").strip()] = float(r["AverageNs"])
     merged = collections.defaultdict(dict)
     for f in sorted(os.listdir(src)):
         if f.endswith("counter_collection.csv"):
@@ -44,8 +62,14 @@ def main():
             e["hbm_bytes_uncorrected"] = e["fetch_bytes_uncorrected"] + e["write_bytes"]
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             e["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0), 4)
+        if "SQ_INSTS_VALU" in d and k in durations:
+            e["avg_ns"] = durations[k]
+            e["valu_issue_frac"] = round(d["SQ_INSTS_VALU"] * 4.0 / (256 * 4) / (durations[k] * 1e-9 * 2.4e9), 4)
         kernels[k] = e
-    stage = [k for k in kernels if k.startswith("stomp::k_rollout")]
+    # the iteration's rollout launch: the k_rollout instantiation with the most dispatches (the
+    # deferred noiseless flush at the end of a run is a different, rare launch)
+    ro = [k for k in kernels if k.startswith("stomp::k_rollout")]
+    stage = [max(ro, key=lambda k: kernels[k].get("dispatches", 0))] if ro else []
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE TCC_HIT_sum TCC_MISS_sum | SQ_* (separate passes), "
                   "bench.py --steps 40 --warmup 5 --no-timing; per-dispatch means",
@@ -54,8 +78,11 @@ def main():
                       "uncalibrated, so the uncorrected figure (x1) is reported beside it: the true bytes lie "
                       "between the two.  KiB -> B; Infinity-Cache hits are counted (memory side of L2), so this is "
                       "L2-miss traffic, an upper bound on HBM bytes",
-        "stage": "rollout_cost = k_rollout",
+        "stage": stage[0] if stage else None,
+        "source_hash": _build.source_hash(),
         "hbm_bytes_per_launch": sum(kernels[k].get("hbm_bytes", 0.0) for k in stage),
+        "valu_insts_per_launch": sum(kernels[k].get("SQ_INSTS_VALU", 0.0) for k in stage),
+        "valu_issue_frac": kernels[stage[0]].get("valu_issue_frac") if stage else None,
         "hbm_bytes_per_launch_uncorrected": sum(kernels[k].get("hbm_bytes_uncorrected", 0.0) for k in stage),
         "kernels": kernels,
     }
