@@ -223,7 +223,7 @@ def bench_problems(args, world, rank, local_rank, dist):
     rng = np.random.default_rng(1234)
     base = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=args.rollouts,
                            num_reused_rollouts=0, build_grid=False)
-    sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
+    sdf = eng.DeviceBuffer(2 * args.grid ** 3, device=local_rank)   # uint16 d2 per voxel
     eng.sdf_build_device(base, sdf.ptr)
     gsize = P if args.group < 0 else args.group
     streams = [eng.Stream(local_rank) for _ in range((P + gsize - 1) // gsize)] if gsize else []
@@ -341,7 +341,7 @@ def main():
     p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid, num_rollouts=K,
                         num_reused_rollouts=args.reused, build_grid=False,
                         max_iterations=args.warmup + 2 * args.steps + 1)
-    sdf = eng.DeviceBuffer(4 * args.grid ** 3, device=local_rank)
+    sdf = eng.DeviceBuffer(2 * args.grid ** 3, device=local_rank)   # uint16 d2 per voxel
     eng.sdf_build_device(p, sdf.ptr)
     comm_id = None
     if world > 1:

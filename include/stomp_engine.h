@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define STOMP_ENGINE_ABI_VERSION 3
+#define STOMP_ENGINE_ABI_VERSION 4
 
 #define STOMP_OK 0
 #define STOMP_E_INVALID (-1)   /* bad sizes / arguments */
@@ -81,14 +81,17 @@ typedef struct stomp_joint {
     double joint_cost;
 } stomp_joint;
 
-/* Distance field: value(x,y,z) = data[(x*ny + y)*nz + z], metres, fp32.  A
- * position maps to the cell round((p - origin)/resolution); cells with any index
- * < 1 or >= n-1 read 0 (distance_field::getDistanceGradient semantics). */
+/* Distance field as PropagationDistanceField holds it (third party; read at
+ * stomp_collision_space.h:187-191): data[(x*ny + y)*nz + z] = d2, the integer squared cell
+ * distance to the nearest obstacle cell, already capped (<= ceil(max_expansion/res)^2); the
+ * distance of a cell is sqrt((double)d2) * resolution, in double, as its sqrt_table_.  A
+ * position maps to the cell round((p - origin)/resolution); cells with any index < 1 or
+ * >= n-1 read distance 0 (distance_field::getDistanceGradient semantics). */
 typedef struct stomp_grid {
     int32_t nx, ny, nz;
     double origin[3];
     double resolution;
-    const float* data;          /* host pointer, or device pointer if data_on_device */
+    const uint16_t* data;       /* host pointer, or device pointer if data_on_device */
     int32_t data_on_device;     /* 1: engine uses the buffer in place (caller keeps it alive) */
 } stomp_grid;
 
@@ -252,15 +255,15 @@ int stomp_engine_set_timing(stomp_engine* e, int32_t enable);
 int stomp_engine_get_timing(stomp_engine* e, const char* name, double* total_ms, int32_t* launches);
 int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count);
 
-/* Distance-field builder (capped, quantised exact EDT):
- *   value = sqrt(min(d2, ceil(max_expansion/res)^2)) * res
+/* Distance-field builder (capped exact EDT, stomp_grid's representation):
+ *   value = min(d2, ceil(max_expansion/res)^2)   (the cap must be <= 255 cells)
  * d2 = integer squared cell distance to the nearest cell whose centre
  * origin + i*res lies in an obstacle.  boxes: n_boxes x (cx,cy,cz,dx,dy,dz),
  * axis-aligned; cylinders: n_cyl x (cx,cy,cz,radius,length), z-aligned.
- * out_device: device buffer of nx*ny*nz floats (z fastest). */
+ * out_device: device buffer of nx*ny*nz uint16 (z fastest). */
 int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
                     double max_expansion, const double* boxes, int32_t n_boxes, const double* cylinders,
-                    int32_t n_cylinders, float* out_device, void* stream);
+                    int32_t n_cylinders, uint16_t* out_device, void* stream);
 
 /* An object of the collision space.  Environment objects are sampled as
  * StompCollisionSpace::addCollisionObjectsToPoints does (stomp_collision_space.cpp:199-297):
@@ -291,12 +294,13 @@ typedef struct stomp_shape {
  * stomp_collision_space.cpp:154-197) on the device: every object's points and the
  * collision-map points (points: n_points x 3, the "points" namespace, :205-211) mark the cell
  * round((p - origin) * (1/res)) when it lies in the grid (PropagationDistanceField::
- * addPointsToField); value = sqrt(min(d2, cap^2)) * res with cap = ceil(max_expansion/res)
- * (<= 255) and d2 the integer squared cell distance to the nearest marked cell.
- * marked (may be NULL): points that landed inside the grid.  Meshes are not supported. */
+ * addPointsToField); value = min(d2, cap^2) with cap = ceil(max_expansion/res) (<= 255) and
+ * d2 the integer squared cell distance to the nearest marked cell (stomp_grid's
+ * representation).  marked (may be NULL): points that landed inside the grid.  Meshes are not
+ * supported. */
 int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
                             double max_expansion, const stomp_shape* shapes, int32_t n_shapes,
-                            const double* points, int64_t n_points, float* out_device, int64_t* marked,
+                            const double* points, int64_t n_points, uint16_t* out_device, int64_t* marked,
                             void* stream);
 
 /* The differentiation stencils the engine is built on (DIFF_RULES of stomp_utils.h:49-56:

@@ -84,9 +84,9 @@ int main(int argc, char** argv)
     }
     fclose(f);
     const size_t cells = (size_t)n * n * n;
-    float* grid = malloc(cells * sizeof(float));
+    unsigned short* grid = malloc(cells * sizeof(unsigned short));   /* d2 per voxel */
     FILE* b = fopen(argv[2], "rb");
-    if (!b || fread(grid, sizeof(float), cells, b) != cells) {
+    if (!b || fread(grid, sizeof(unsigned short), cells, b) != cells) {
         fprintf(stderr, "cannot read the field\n");
         return 2;
     }

@@ -30,7 +30,7 @@ class so_joint(C.Structure):
 
 class so_sdf(C.Structure):
     _fields_ = [("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("origin", C.c_double * 3),
-                ("resolution", C.c_double), ("data", C.POINTER(C.c_float))]
+                ("resolution", C.c_double), ("data", C.POINTER(C.c_uint16))]
 
 
 class so_inertia(C.Structure):
@@ -117,9 +117,10 @@ def lib():
         l.so_sdf_build_objects.restype = C.c_longlong
         l.so_sdf_build_objects.argtypes = [C.c_int, C.c_int, C.c_int, dp, C.c_double, C.c_double,
                                            C.POINTER(so_shape), C.c_int, dp, C.c_longlong,
-                                           C.POINTER(C.c_ubyte), C.POINTER(C.c_float)]
+                                           C.POINTER(C.c_ubyte), C.POINTER(C.c_uint16)]
+        l.so_sdf_from_occupancy.restype = C.c_int
         l.so_sdf_from_occupancy.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
-                                            C.POINTER(C.c_ubyte), C.POINTER(C.c_float)]
+                                            C.POINTER(C.c_ubyte), C.POINTER(C.c_uint16)]
         _lib = l
     return _lib
 
@@ -130,7 +131,7 @@ class so_shape(C.Structure):
 
 
 def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
-    """so_sdf_build_objects (oracle/sdf_oracle.c) for problem.Grid `grid`: (field n^3 fp32 or None,
+    """so_sdf_build_objects (oracle/sdf_oracle.c) for problem.Grid `grid`: (field n^3 uint16 squared cell distances or None,
     marks n^3 uint8, number of points marked)."""
     n = grid.n
     arr = (so_shape * max(len(objects), 1))()
@@ -142,12 +143,12 @@ def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
         arr[i].dims[:] = [float(v) for v in d[:3]]
     pts = np.ascontiguousarray(points if points is not None else np.zeros((0, 3)), np.float64).reshape(-1, 3)
     occ = np.zeros((n, n, n), np.uint8)
-    field = np.zeros((n, n, n), np.float32) if with_field else None
+    field = np.zeros((n, n, n), np.uint16) if with_field else None
     origin = np.array(grid.origin, np.float64)
     marked = lib().so_sdf_build_objects(
         n, n, n, _dp(origin), grid.resolution, grid.max_expansion, arr, len(objects),
         _dp(pts if pts.size else np.zeros(3)), len(pts), occ.ctypes.data_as(C.POINTER(C.c_ubyte)),
-        field.ctypes.data_as(C.POINTER(C.c_float)) if field is not None else None)
+        field.ctypes.data_as(C.POINTER(C.c_uint16)) if field is not None else None)
     if marked < 0:
         raise ValueError("so_sdf_build_objects: invalid input")
     return field, occ, int(marked)
@@ -155,9 +156,10 @@ def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
 
 def sdf_from_occupancy(occ: np.ndarray, resolution: float, max_expansion: float) -> np.ndarray:
     occ = np.ascontiguousarray(occ, np.uint8)
-    out = np.zeros(occ.shape, np.float32)
-    lib().so_sdf_from_occupancy(*occ.shape, resolution, max_expansion, occ.ctypes.data_as(C.POINTER(C.c_ubyte)),
-                                out.ctypes.data_as(C.POINTER(C.c_float)))
+    out = np.zeros(occ.shape, np.uint16)
+    if lib().so_sdf_from_occupancy(*occ.shape, resolution, max_expansion, occ.ctypes.data_as(C.POINTER(C.c_ubyte)),
+                                   out.ctypes.data_as(C.POINTER(C.c_uint16))) != 0:
+        raise ValueError("so_sdf_from_occupancy: cap above 255 cells")
     return out
 
 
@@ -190,7 +192,7 @@ class Oracle:
         self._sph = _arr([so_sphere(s.segment, s.radius, s.clearance, (C.c_double * 3)(*s.pos)) for s in p.spheres],
                          so_sphere)
         self._joints = _arr([so_joint(int(j.has_limits), j.min, j.max, j.joint_cost) for j in p.robot.joints], so_joint)
-        self._sdf = np.ascontiguousarray(p.sdf, dtype=np.float32)
+        self._sdf = np.ascontiguousarray(p.sdf, dtype=np.uint16)
         pr = p.params
         self._sig = pr.per_joint("noise_stddev", self.J)
         self._dec = pr.per_joint("noise_decay", self.J)
@@ -206,7 +208,7 @@ class Oracle:
         cfg.spheres = self._sph
         cfg.joints = self._joints
         cfg.sdf = so_sdf(g.n, g.n, g.n, (C.c_double * 3)(*g.origin), g.resolution,
-                         self._sdf.ctypes.data_as(C.POINTER(C.c_float)))
+                         self._sdf.ctypes.data_as(C.POINTER(C.c_uint16)))
         cfg.discretization = pr.trajectory_discretization
         cfg.smoothness_costs = (C.c_double * 3)(pr.smoothness_cost_velocity, pr.smoothness_cost_acceleration,
                                                 pr.smoothness_cost_jerk)

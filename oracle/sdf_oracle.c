@@ -21,8 +21,9 @@
  *     vendored: points exactly on a surface are parity unpinned).
  *  3. distance_field::PropagationDistanceField::addPointsToField (third party): every point
  *     marks the cell round((p - origin) * (1/res)) when all three indices are in [0, n); the
- *     field is the capped exact EDT to the marked cells, value = sqrt(min(d2, cap^2)) * res,
- *     cap = ceil(max_expansion / res), d2 the integer squared cell distance.  The reference's
+ *     field is the capped exact EDT to the marked cells, stored as min(d2, cap^2) with
+ *     cap = ceil(max_expansion / res) and d2 the integer squared cell distance (the field's
+ *     distance_square_; its distance is sqrt_table_[d2] = sqrt(d2) * res).  The reference's
  *     own propagation (a 26-neighbour closest-point wavefront) can differ from the exact EDT
  *     by a fraction of a cell far from the obstacles: PARITY UNPINNED.
  *
@@ -176,10 +177,11 @@ static void robot_body(marker* mk, const so_shape* s, double res)
  * a window of |dy| <= cap along y and |dx| <= cap along x).  A window term needs its component
  * <= cap to reach a value <= cap^2, so the windowed minimum is exact wherever the result is
  * below the cap, and anything above is clamped to it. */
-void so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,
-                           float* sdf)
+int so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,
+                          unsigned short* sdf)
 {
     const int cap = (int)ceil(max_expansion / res);
+    if (cap < 0 || cap > 255) return -1;
     const long long cap2 = (long long)cap * cap, far = cap2 + 1;
     const size_t n = (size_t)nx * ny * nz;
     long long* a = (long long*)malloc(n * sizeof(long long));
@@ -220,17 +222,19 @@ void so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expans
                     if (v < best) best = v;
                 }
                 const long long d2 = best < cap2 ? best : cap2;
-                sdf[((size_t)x * ny + y) * nz + z] = (float)(sqrt((double)d2) * res);
+                sdf[((size_t)x * ny + y) * nz + z] = (unsigned short)d2;
             }
     free(a);
     free(b);
+    return 0;
 }
 
 long long so_sdf_build_objects(int nx, int ny, int nz, const double* origin, double res, double max_expansion,
                                const so_shape* shapes, int n_shapes, const double* points, long long n_points,
-                               unsigned char* occ, float* sdf)
+                               unsigned char* occ, unsigned short* sdf)
 {
     if (nx <= 0 || ny <= 0 || nz <= 0 || !(res > 0)) return -1;
+    if (sdf && !(ceil(max_expansion / res) <= 255.0)) return -1;
     const size_t n = (size_t)nx * ny * nz;
     unsigned char* own = NULL;
     if (!occ && sdf) occ = own = (unsigned char*)malloc(n);

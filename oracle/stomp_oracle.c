@@ -633,7 +633,10 @@ double so_sdf_distance(const so_problem* P, double x, double y, double z)
           fz < (double)(g->nz - 1)))
         return 0.0;
     long ix = (long)fx, iy = (long)fy, iz = (long)fz;
-    return (double)g->data[((size_t)ix * g->ny + (size_t)iy) * g->nz + (size_t)iz];
+    /* PropagationDistanceField::getDistance: sqrt_table_[distance_square_], the table made as
+     * sqrt(double(i)) * resolution */
+    const unsigned d2 = g->data[((size_t)ix * g->ny + (size_t)iy) * g->nz + (size_t)iz];
+    return sqrt((double)d2) * g->resolution;
 }
 
 /* stomp_collision_space.h:193-228 (gradient is CHOMP-only and not computed) */

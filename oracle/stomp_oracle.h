@@ -59,12 +59,14 @@ typedef struct {
     double joint_cost;  /* joint_costs/<name>, default 1.0 (stomp_optimizer.cpp:107-109) */
 } so_joint;
 
-/* Voxel grid, z fastest: value(x,y,z) = data[(x*ny + y)*nz + z] (metres, fp32) */
+/* Voxel grid, z fastest: data[(x*ny + y)*nz + z] = d2, the squared cell distance to the nearest
+ * obstacle cell (capped).  The distance is sqrt((double)d2) * resolution, the value
+ * PropagationDistanceField reads from its sqrt_table_ (third party; distance_square_ per voxel) */
 typedef struct {
     int nx, ny, nz;
     double origin[3];
     double resolution;
-    const float* data;
+    const unsigned short* data;
 } so_sdf;
 
 /* KDL::RigidBodyInertia(m, cog, Ic) of a segment, in the segment frame; Ic is about the
@@ -206,14 +208,16 @@ typedef struct {
     double orientation[4];   /* quaternion x, y, z, w */
     double dims[3];
 } so_shape;
-/* occ (nx*ny*nz bytes, may be NULL) receives the marked cells; sdf (floats, may be NULL) the
- * field sqrt(min(d2, cap^2)) * res.  Returns the number of points marked (inside the grid). */
+/* occ (nx*ny*nz bytes, may be NULL) receives the marked cells; sdf (uint16, may be NULL) the
+ * field min(d2, cap^2), cap = ceil(max_expansion / res) <= 255.  Returns the number of points
+ * marked (inside the grid), -1 on invalid input. */
 long long so_sdf_build_objects(int nx, int ny, int nz, const double* origin, double res, double max_expansion,
                                const so_shape* shapes, int n_shapes, const double* points, long long n_points,
-                               unsigned char* occ, float* sdf);
-/* capped EDT of an occupancy grid alone (the second half of so_sdf_build_objects) */
-void so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,
-                           float* sdf);
+                               unsigned char* occ, unsigned short* sdf);
+/* capped EDT of an occupancy grid alone (the second half of so_sdf_build_objects); -1 when the
+ * cap exceeds 255 cells (d2 would not fit 16 bits) */
+int so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,
+                          unsigned short* sdf);
 
 #ifdef __cplusplus
 }

@@ -126,7 +126,8 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // one value where floor(u + 0.5) != round(u) for u >= 0, u = 0.5 - 2^-54, is below 0.5 and
 // rejected by the range test).  So the range test moves onto u and each axis costs sub, mul,
 // two compares, add and floor.
-__device__ __forceinline__ float sdf_distance(const DevModel& m, const double* __restrict__ p)
+// Returns the voxel's squared cell distance d2 (0 outside: distance 0).
+__device__ __forceinline__ unsigned sdf_d2(const DevModel& m, const double* __restrict__ p)
 {
     const double ux = (p[0] - m.ox) * m.inv_res;
     const double uy = (p[1] - m.oy) * m.inv_res;
@@ -134,8 +135,14 @@ __device__ __forceinline__ float sdf_distance(const DevModel& m, const double* _
     const bool ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
     const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
     const unsigned idx = (unsigned)(ok ? cell : 0.0);
-    const float v = m.sdf[idx];
-    return ok ? v : 0.0f;
+    const unsigned v = m.sdf[idx];
+    return ok ? v : 0u;
+}
+
+// PropagationDistanceField::getDistance: sqrt_table_[d2], the table made as sqrt(double(i)) * resolution
+__device__ __forceinline__ double sdf_metres(const DevModel& m, unsigned d2)
+{
+    return sqrt((double)d2) * m.res;
 }
 
 // StompCollisionSpace::getCollisionPointPotentialGradient (stomp_collision_space.h:193-228)

@@ -130,7 +130,7 @@ struct stomp_engine {
     double *d_tot_loc = nullptr, *d_tot_all = nullptr, *d_tot_x = nullptr, *d_slot = nullptr, *d_slot_all = nullptr;
     int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
-    float* d_sdf = nullptr;
+    uint16_t* d_sdf = nullptr;   // d2 per voxel
     int* d_pad_cf = nullptr;
     int pad_collision = 0;
     bool reused_next = false, extra_added = false;
@@ -820,6 +820,33 @@ const char* stomp_last_error(void) { return g_last_error.c_str(); }
 
 const char* stomp_engine_last_error(const stomp_engine* e) { return e ? e->err.c_str() : g_last_error.c_str(); }
 
+// The hinge potential's zero case and the collision test of StompCollisionSpace::
+// getCollisionPointPotentialGradient (stomp_collision_space.h:193-228) as thresholds on a voxel's
+// squared cell distance d2, whose distance is sqrt((double)d2) * res (the field's sqrt_table_):
+//   potential == 0  <=>  d2 >= zero_lim      in collision  <=>  d2 < col_lim
+// Every d2 a 16-bit voxel can hold is priced with the reference's expressions (one rounding per
+// operation, as the kernel's), and each predicate is checked to switch exactly once, so the
+// kernel's integer compares give the same answers as the potential itself.
+static bool sphere_thresholds(double radius, double clearance, double res, int* zero_lim, int* col_lim)
+{
+    if (!(radius >= 0.0 && clearance > 0.0 && std::isfinite(radius) && std::isfinite(clearance))) return false;
+    int zl = 65536, cl = 65536;
+    bool zseen = false, cseen = false;
+    for (int d2 = 0; d2 <= 65535; ++d2) {
+        const double dist = std::sqrt((double)d2) * res;
+        const double dd = dist - radius;
+        const bool zero = dd >= clearance;
+        const bool col = dist <= radius;
+        if (zero && !zseen) { zl = d2; zseen = true; }
+        if (!zero && zseen) return false;
+        if (!col && !cseen) { cl = d2; cseen = true; }
+        if (col && cseen) return false;
+    }
+    *zero_lim = zl;
+    *col_lim = cl;
+    return true;
+}
+
 int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
 {
     if (!d || !out) return fail(nullptr, STOMP_E_INVALID, "null argument");
@@ -848,9 +875,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     for (int s = 0; s < d->num_segments; ++s)
         if (d->segments[s].parent >= s || d->segments[s].q_index >= d->num_joints)
             return fail(nullptr, STOMP_E_INVALID, "segment %d: parent must precede it (DFS order), q_index < J", s);
-    for (int j = 0; j < d->num_spheres; ++j)
+    for (int j = 0; j < d->num_spheres; ++j) {
         if (d->spheres[j].segment < 0 || d->spheres[j].segment >= d->num_segments)
             return fail(nullptr, STOMP_E_INVALID, "sphere %d: bad segment", j);
+        int zl, cl;
+        if (!sphere_thresholds(d->spheres[j].radius, d->spheres[j].clearance, d->grid.resolution, &zl, &cl))
+            return fail(nullptr, STOMP_E_INVALID, "sphere %d: radius / clearance not finite and positive", j);
+    }
     if (d->torque_cost_weight > 1e-9) {
         std::vector<int> path;
         if (const char* why = torque_chain(d, path)) return fail(nullptr, STOMP_E_UNSUPPORTED, "%s", why);
@@ -959,10 +990,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     std::vector<DevSphere> sph(std::max(e->S, 1));
     for (int j = 0; j < e->S; ++j) {
         const stomp_sphere& g = d->spheres[j];
-        sph[j].segment = g.segment; sph[j].slot = e->sphere_slot[j];
+        sph[j].slot = e->sphere_slot[j];
         sph[j].radius = g.radius; sph[j].clearance = g.clearance;
         sph[j].inv_clearance = 1.0 / g.clearance;   // stomp_collision_point.cpp:50
         std::memcpy(sph[j].pos, g.pos, sizeof g.pos);
+        sphere_thresholds(g.radius, g.clearance, d->grid.resolution, &sph[j].zero_lim, &sph[j].col_lim);
+        sph[j].pad_ = 0;
     }
     std::vector<int> has_lim(J);
     std::vector<double> jmin(J), jmax(J);
@@ -982,7 +1015,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(upload(e, &e->d_goal, e->goal.data(), e->goal.size()));
     const size_t ncell = (size_t)d->grid.nx * d->grid.ny * d->grid.nz;
     if (d->grid.data_on_device) {
-        e->d_sdf = (float*)d->grid.data;
+        e->d_sdf = (uint16_t*)d->grid.data;
     } else {
         CREATE_TRY(upload(e, &e->d_sdf, d->grid.data, ncell));
     }
@@ -1784,11 +1817,13 @@ int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
 }
 
 int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double res, double max_expansion,
-                    const double* boxes, int32_t n_boxes, const double* cyl, int32_t n_cyl, float* out, void* stream)
+                    const double* boxes, int32_t n_boxes, const double* cyl, int32_t n_cyl, uint16_t* out, void* stream)
 {
     if (nx <= 0 || ny <= 0 || nz <= 0 || !(res > 0) || !out) return fail(nullptr, STOMP_E_INVALID, "invalid grid");
     const int n[3] = {nx, ny, nz};
-    const int cap = (int)std::ceil(max_expansion / res);
+    const double capd = std::ceil(max_expansion / res);
+    if (!(capd >= 0) || capd > 255) return fail(nullptr, STOMP_E_UNSUPPORTED, "max_expansion / resolution above 255 cells");
+    const int cap = (int)capd;
     const int cap2 = cap * cap;
     auto range = [&](double lo, double hi, int a, int& i0, int& i1) {
         i0 = std::max((int)std::ceil((lo - origin[a]) / res), 0);
@@ -1854,7 +1889,7 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
         if (d_z) hipFree(d_z);
         return fail(nullptr, STOMP_E_DEVICE, "sdf build: %s", hipGetErrorString(cp));
     }
-    launch_sdf_build(nx, ny, nz, cap2, res, d_b, (int)br.size() / 6, d_c, d_z, (int)cz.size() / 2, out, s);
+    launch_sdf_build(nx, ny, nz, cap2, d_b, (int)br.size() / 6, d_c, d_z, (int)cz.size() / 2, out, s);
     hipError_t st = hipStreamSynchronize(s);
     if (d_b) hipFree(d_b);
     if (d_c) hipFree(d_c);
@@ -1868,7 +1903,7 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
 // own running-sum loops), the marking and the EDT run on the device (k_sdf.hip)
 int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* origin, double res,
                             double max_expansion, const stomp_shape* shapes, int32_t n_shapes, const double* points,
-                            int64_t n_points, float* out, int64_t* marked, void* stream)
+                            int64_t n_points, uint16_t* out, int64_t* marked, void* stream)
 {
     if (nx <= 0 || ny <= 0 || nz <= 0 || !(res > 0) || !out || !origin || n_shapes < 0 || n_points < 0 ||
         (n_shapes > 0 && !shapes) || (n_points > 0 && !points))
@@ -1995,7 +2030,7 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
     g.marked = d_marked;
     launch_mark_points(d_pts, n_points, g, st);
     for (const SdfLatticeJob& j : jobs) launch_mark_lattice(j, d_axes, g, st);
-    launch_edt(nx, ny, nz, cap, occ, a, b, out, res, st);
+    launch_edt(nx, ny, nz, cap, occ, a, b, out, st);
     unsigned long long nm = 0;
     err = hipGetLastError();
     if (err == hipSuccess) err = hipMemcpyAsync(&nm, d_marked, sizeof nm, hipMemcpyDeviceToHost, st);

@@ -9,11 +9,13 @@
 //      segments in DFS order.  Each sphere-carrying segment ("slot") is published to an LDS
 //      frame buffer [12][N]; then lane (t, g) reads the frame at t once and takes spheres
 //      g, g + G, ... of the slot (G = 256 / N groups): sphere position
-//      (stomp_collision_point.h:138-141), distance-field gathers (branch-free, 4 in flight
-//      per lane) and hinge potential (stomp_optimizer.cpp:659-674,
-//      stomp_collision_space.h:193-228); where the potential is non-zero, the 7-tap
-//      velocity (:683-698) from the neighbouring frames in LDS (padding rows: iteration-0
-//      FK of start/goal) and a = pot * |v|; then lanes t fold a over the slot's spheres,
+//      (stomp_collision_point.h:138-141), distance-field gathers of the voxel's squared cell
+//      distance d2 (branch-free, all in flight per lane); the hinge potential is zero and the
+//      collision flag set by per-sphere thresholds on d2 (stomp_optimizer.cpp:659-674,
+//      stomp_collision_space.h:193-228); where the potential is non-zero, the distance
+//      sqrt(d2) res, the potential, the 7-tap velocity (:683-698) from the neighbouring frames
+//      in LDS (padding rows: iteration-0 FK of start/goal) and a = pot * |v|; then lanes t
+//      fold a over the slot's spheres,
 //      in list order, into cum / state (:1096-1105).  Slots are numbered in sphere order,
 //      so slot-by-slot folding is the reference's order.
 //   3. costs(t) = w_obs * state (:1148-1151), the collision flag and the total (:1155).
@@ -414,7 +416,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double F[12];
             int fslot = -1;
             for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
-                float dv[kLaneSpheres];
+                unsigned dv[kLaneSpheres];
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
@@ -430,22 +432,23 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
                     for (int i = 0; i < 3; ++i)
                         x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
-                    dv[u] = sdf_distance(m, x);
+                    dv[u] = sdf_d2(m, x);
                 }
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
                     const int sq = pg * CPL + u0 + u;
                     const bool in = sq < S;
-                    double pot = 0.0;
+                    bool nz = false;
                     if (in) {
                         const DevSphere& sp = sph[sq];
-                        const double dd = (double)dv[u];
-                        col |= dd <= sp.radius;
-                        pot = potential(sp, dd);
-                        av[sq * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                        const int d2 = (int)dv[u];
+                        col |= d2 < sp.col_lim;
+                        nz = d2 < sp.zero_lim;
+                        // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
+                        // is +0 exactly when pot == +0
+                        av[sq * N + pt] = nz ? (double)d2 : 0.0;
                     }
-                    const bool nz = in && pot != 0.0;
                     const unsigned long long mask = __ballot(nz);
                     if (mask) {
                         const int lane_id = tid & 63;
@@ -465,7 +468,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             const int it = nzl[i];
             const int qi = it / N, ti = it - qi * N;
             const DevSphere& sp = sph[qi];
-            av[it] *= sphere_speed(m, fb + (size_t)sp.slot * 12 * N, pad, sp, qi, ti);
+            const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
+            av[it] = pot * sphere_speed(m, fb + (size_t)sp.slot * 12 * N, pad, sp, qi, ti);
         }
         __syncthreads();   // every a value complete
         STAMP(12);
@@ -520,7 +524,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double F[12];
 #pragma unroll
             for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
-            float dv[kLaneSpheres];
+            unsigned dv[kLaneSpheres];
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform
@@ -529,7 +533,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
                     x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
-                dv[u] = sdf_distance(m, x);
+                dv[u] = sdf_d2(m, x);
             }
             STAMP(40 + run);
 #pragma unroll
@@ -537,15 +541,16 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 if (u * G >= ns) break;   // uniform
                 const int q = pg + u * G;
                 const bool in = q < ns;
-                double pot = 0.0;
+                bool nz = false;
                 if (in) {
                     const DevSphere& sp = sph[sb + q];
-                    const double dd = (double)dv[u];
-                    col |= dd <= sp.radius;
-                    pot = potential(sp, dd);
-                    av[q * N + pt] = pot;   // a = pot * |v| is +0 exactly when pot == +0
+                    const int d2 = (int)dv[u];
+                    col |= d2 < sp.col_lim;
+                    nz = d2 < sp.zero_lim;
+                    // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
+                    // is +0 exactly when pot == +0
+                    av[q * N + pt] = nz ? (double)d2 : 0.0;
                 }
-                const bool nz = in && pot != 0.0;
                 const unsigned long long mask = __ballot(nz);
                 if (mask) {
                     const int lane_id = tid & 63;
@@ -565,7 +570,9 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         for (int i = tid; i < nz_count; i += BLOCK) {
             const int it = nzl[i];
             const int qi = it / N, ti = it - qi * N;
-            av[it] *= sphere_speed(m, fb, pad, sph[sb + qi], sb + qi, ti);
+            const DevSphere& sp = sph[sb + qi];
+            const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
+            av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
         }
         // C is reloaded from fb (not kept live across the pairs)
         if (fk_lane) {

@@ -62,7 +62,7 @@ __global__ void k_pad_fk(DevModel m, const double* start, const double* goal, do
         for (int s = o.sph_begin; s < o.sph_end; ++s) {
             double p[3];
             apply(C.R, C.p, m.sph[s].pos, p);
-            if ((double)sdf_distance(m, p) <= m.sph[s].radius) col = true;
+            if ((int)sdf_d2(m, p) < m.sph[s].col_lim) col = true;   // distance <= radius
             for (int row = 0; row < 6; ++row)
                 for (int c = 0; c < 3; ++c) pad_pos[((size_t)(side * 6 + row) * m.S + s) * 3 + c] = p[c];
         }
@@ -421,8 +421,8 @@ void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, cons
 }
 
 // ============================================================== distance field construction
-__global__ void k_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes, int nb,
-                            const long long* cyl_d2, const int* cyl_z, int nc, float* out)
+__global__ void k_sdf_build(int nx, int ny, int nz, int cap2, const int* boxes, int nb, const long long* cyl_d2,
+                            const int* cyl_z, int nc, unsigned short* out)
 {
     const long long total = (long long)nx * ny * nz;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -445,15 +445,14 @@ __global__ void k_sdf_build(int nx, int ny, int nz, int cap2, double res, const 
             long long v = dxy + dz * dz;
             if (v < d2) d2 = v;
         }
-        out[idx] = (float)(sqrt((double)d2) * res);
+        out[idx] = (unsigned short)d2;   // <= cap2 <= 65535
     }
 }
 
-void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes, int nb, const long long* cyl_d2,
-                      const int* cyl_z, int nc, float* out, hipStream_t s)
+void launch_sdf_build(int nx, int ny, int nz, int cap2, const int* boxes, int nb, const long long* cyl_d2,
+                      const int* cyl_z, int nc, unsigned short* out, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_sdf_build, dim3(2048), dim3(256), 0, s, nx, ny, nz, cap2, res, boxes, nb, cyl_d2, cyl_z, nc,
-                       out);
+    hipLaunchKernelGGL(k_sdf_build, dim3(2048), dim3(256), 0, s, nx, ny, nz, cap2, boxes, nb, cyl_d2, cyl_z, nc, out);
 }
 
 }  // namespace stomp

@@ -11,7 +11,7 @@
 //   k_edt_window    the capped exact EDT as three windowed minima (z from the marks, then y, then
 //                   x), one lane per cell with the window along the axis; the lanes of a wave are
 //                   consecutive z, so every window read is a coalesced row; the last pass writes
-//                   sqrt(min(d2, cap^2)) * res
+//                   min(d2, cap^2), the field's squared cell distance (distance = sqrt(d2) * res)
 // oracle/sdf_oracle.c restates the same rules (with a sweep for the z pass); the tests compare the
 // fields bit for bit.
 #include "kernels.h"
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void k_mark_points(const double* pts, long lon
 // The z pass reads the marks (0 for a marked cell, far otherwise); the x pass writes the field.
 template <int AXIS, bool FROM_OCC, bool FINAL>
 __global__ __launch_bounds__(256) void k_edt_window(int nx, int ny, int nz, int cap, const void* in_raw,
-                                                    unsigned short* out, float* field, double res)
+                                                    unsigned short* out)
 {
     const long long total = (long long)nx * ny * nz;
     const long long idx = blockIdx.x * 256LL + threadIdx.x;
@@ -141,12 +141,7 @@ __global__ __launch_bounds__(256) void k_edt_window(int nx, int ny, int nz, int 
             best = v < best ? v : best;
         }
     }
-    if (FINAL) {
-        const int d2 = best < far - 1 ? best : far - 1;   // min(d2, cap^2)
-        field[idx] = (float)(sqrt((double)d2) * res);
-    } else {
-        out[idx] = (unsigned short)best;
-    }
+    out[idx] = (unsigned short)(FINAL && best > far - 1 ? far - 1 : best);   // the last pass: min(d2, cap^2)
 }
 
 void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMarkArgs& g, hipStream_t s)
@@ -163,16 +158,13 @@ void launch_mark_points(const double* pts, long long np, const SdfMarkArgs& g, h
 }
 
 void launch_edt(int nx, int ny, int nz, int cap, const unsigned char* occ, unsigned short* a, unsigned short* b,
-                float* field, double res, hipStream_t s)
+                unsigned short* field, hipStream_t s)
 {
     const long long total = (long long)nx * ny * nz;
     const dim3 grid((unsigned)((total + 255) / 256));
-    hipLaunchKernelGGL((k_edt_window<2, true, false>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)occ, a,
-                       (float*)nullptr, res);
-    hipLaunchKernelGGL((k_edt_window<1, false, false>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)a, b,
-                       (float*)nullptr, res);
-    hipLaunchKernelGGL((k_edt_window<0, false, true>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)b,
-                       (unsigned short*)nullptr, field, res);
+    hipLaunchKernelGGL((k_edt_window<2, true, false>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)occ, a);
+    hipLaunchKernelGGL((k_edt_window<1, false, false>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)a, b);
+    hipLaunchKernelGGL((k_edt_window<0, false, true>), grid, dim3(256), 0, s, nx, ny, nz, cap, (const void*)b, field);
 }
 
 }  // namespace stomp

@@ -8,7 +8,8 @@
 //   params, noise,
 //   control, prob    [K_loc][J][N]         fp64  Rollout::parameters_/noise_/control_costs_/probabilities_
 //   state            [K_loc][N]            fp64  Rollout::state_costs_
-//   sdf              [nx][ny][nz]          fp32  distance field (z fastest)
+//   sdf              [nx][ny][nz]          u16   distance field as squared cell distances d2 (z
+//                                                fastest); distance = sqrt((double)d2) * res
 //   psum/u partials  [blocks][J][N]        fp64  per-64-rollout-block sums (RCCL all-gather payload)
 #pragma once
 
@@ -47,7 +48,12 @@ struct DevSegment {
 };
 
 struct DevSphere {
-    int segment, slot;          // slot: index of its segment's published frame
+    int slot;                   // index of its segment's published frame
+    // the hinge potential and the collision test as thresholds on the voxel's d2 (made on the
+    // host with the potential's own expressions, stomp_collision_space.h:193-228):
+    //   potential == 0   <=>  d2 >= zero_lim   (d = sqrt(d2) res - radius >= clearance)
+    //   in collision     <=>  d2 <  col_lim    (sqrt(d2) res <= radius)
+    int zero_lim, col_lim, pad_;
     double radius, clearance, inv_clearance;
     double pos[3];
 };
@@ -75,10 +81,10 @@ struct DevModel {
     const FkOp* ops;
     const int* slot_sph;        // [nslots+1] spheres of slot g: [slot_sph[g], slot_sph[g+1])
     const double* pad_pos;      // [12][S][3]
-    const float* sdf;
+    const unsigned short* sdf;  // d2 per voxel
     int nx, ny, nz;
     double ox, oy, oz, res, inv_res;
-    double ny_d, nz_d;          // ny, nz as doubles (the fp64 cell index of sdf_distance)
+    double ny_d, nz_d;          // ny, nz as doubles (the fp64 cell index of sdf_d2)
     double hi_x, hi_y, hi_z;    // n - 1.5 per axis: round(u) <= n - 2 <=> u < n - 1.5
     const double* start;        // [J]
     const double* goal;         // [J]
@@ -348,9 +354,9 @@ void launch_reuse_pack(int Kr, int J, int N, int first, int K_loc, const int* se
 void launch_reuse_unpack(int Kr, int K_gen, int J, int N, int first, int K_loc, const int* sel,
                          const double* slot_all, const double* x_params, const double* x_state, const double* theta,
                          double* params, double* noise, double* state, const int* stop, hipStream_t s);
-void launch_sdf_build(int nx, int ny, int nz, int cap2, double res, const int* boxes /*n x 6 idx ranges*/,
-                      int nb, const long long* cyl_d2 /*nc x nx x ny*/, const int* cyl_z /*nc x 2*/, int nc,
-                      float* out, hipStream_t s);
+void launch_sdf_build(int nx, int ny, int nz, int cap2, const int* boxes /*n x 6 idx ranges*/, int nb,
+                      const long long* cyl_d2 /*nc x nx x ny*/, const int* cyl_z /*nc x 2*/, int nc,
+                      unsigned short* out, hipStream_t s);
 
 // the reference's object voxeliser (k_sdf.hip); shape types as STOMP_SHAPE_* / STOMP_BODY_*
 constexpr int kShapeBox = 0, kShapeCylinder = 1, kBodySphere = 2, kBodyBox = 3, kBodyCylinder = 4;
@@ -374,6 +380,6 @@ struct SdfLatticeJob {
 void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMarkArgs& g, hipStream_t s);
 void launch_mark_points(const double* pts, long long np, const SdfMarkArgs& g, hipStream_t s);
 void launch_edt(int nx, int ny, int nz, int cap, const unsigned char* occ, unsigned short* a, unsigned short* b,
-                float* field, double res, hipStream_t s);
+                unsigned short* field, hipStream_t s);
 
 }  // namespace stomp

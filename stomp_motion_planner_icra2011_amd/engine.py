@@ -14,7 +14,7 @@ import numpy as np
 from . import _build
 
 _LIB_PATH = _build.LIB
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class stomp_segment(C.Structure):
@@ -172,7 +172,8 @@ def _check(rc: int, handle=None):
 
 
 def sdf_build_device(problem, device_tensor_ptr: int, stream: int = 0):
-    """Builds problem.grid's distance field directly into a device buffer of n^3 floats."""
+    """Builds problem.grid's distance field directly into a device buffer of n^3 uint16 squared cell
+    distances (stomp_grid's representation; problem.build_sdf is the host twin)."""
     l = load_library()
     g = problem.grid
     boxes = np.array([list(b.center) + list(b.dims) for b in problem.boxes], np.float64).reshape(-1)
@@ -200,7 +201,7 @@ def shape_array(objects):
 def sdf_build_objects_device(grid, objects, device_ptr: int, points=None, stream: int = 0) -> int:
     """The reference's distance-field fill (stomp_sdf_build_objects) of problem.Grid `grid` from
     collision objects (problem.SceneObject) and collision-map points (P x 3) into a device buffer
-    of n^3 floats.  Returns the number of points that landed in the grid."""
+    of n^3 uint16 squared cell distances.  Returns the number of points that landed in the grid."""
     l = load_library()
     origin = np.array(grid.origin, np.float64)
     pts = np.ascontiguousarray(points if points is not None else np.zeros((0, 3)), np.float64).reshape(-1, 3)
@@ -246,7 +247,7 @@ class Engine:
         if sdf_device_ptr is not None:
             grid_ptr, on_dev = sdf_device_ptr, 1
         else:
-            self._sdf = np.ascontiguousarray(p.sdf, np.float32)
+            self._sdf = np.ascontiguousarray(p.sdf, np.uint16)
             grid_ptr, on_dev = self._sdf.ctypes.data, 0
         d.grid = stomp_grid(g.n, g.n, g.n, (C.c_double * 3)(*g.origin), g.resolution, C.c_void_p(grid_ptr), on_dev)
         d.discretization = pr.trajectory_discretization

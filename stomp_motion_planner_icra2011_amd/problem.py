@@ -325,7 +325,9 @@ def cylinder_disc_d2(c: Cylinder, grid: Grid) -> np.ndarray:
 
 
 def build_sdf(grid: Grid, boxes, cylinders) -> np.ndarray:
-    """Capped quantised distance field, fp32, shape (n, n, n), index [x, y, z] (z fastest)."""
+    """Capped distance field as squared cell distances: uint16 d2 = min(d2, cap^2), shape (n, n, n),
+    index [x, y, z] (z fastest).  The distance of a cell is sqrt(d2) * res (sdf_metres): the
+    integer distance_square_ and sqrt_table_ of PropagationDistanceField."""
     n, res = grid.n, grid.resolution
     cap = grid.max_dist_int
     cap2 = cap * cap
@@ -350,9 +352,15 @@ def build_sdf(grid: Grid, boxes, cylinders) -> np.ndarray:
             continue
         dz = _axis_d2(z0, z1, n)
         np.minimum(d2, np.minimum(dxy[:, :, None] + dz[None, None, :], cap2), out=d2)
-    d2 = np.minimum(d2, cap2)
-    table = np.sqrt(np.arange(cap2 + 1, dtype=np.float64)) * res
-    return table[d2].astype(np.float32)
+    if cap2 > 65535:
+        raise ValueError("max_expansion / resolution above 255 cells: d2 does not fit 16 bits")
+    return np.minimum(d2, cap2).astype(np.uint16)
+
+
+def sdf_metres(grid: Grid, d2: np.ndarray) -> np.ndarray:
+    """Distance in metres of squared cell distances: sqrt(double(d2)) * resolution, PropagationDistanceField's
+    sqrt_table_ (third party; call site stomp_collision_space.h:187-191)."""
+    return np.sqrt(np.asarray(d2, np.float64)) * grid.resolution
 
 
 # ----------------------------------------------------------------- parameters
@@ -524,5 +532,5 @@ def sdf_lookup(p: Problem, pos: np.ndarray) -> np.ndarray:
     f = c_round((pos - np.array(g.origin)) * (1.0 / g.resolution))
     ok = np.all((f >= 1) & (f < g.n - 1), axis=-1)
     idx = np.where(ok[..., None], f, 0).astype(np.int64)
-    d = p.sdf[idx[..., 0], idx[..., 1], idx[..., 2]].astype(np.float64)
+    d = sdf_metres(g, p.sdf[idx[..., 0], idx[..., 1], idx[..., 2]])
     return np.where(ok, d, 0.0)

@@ -34,7 +34,7 @@ struct Problem {
     StompRobotModel robot;
     StompTrajectory traj;
     StompCollisionSpace space;
-    std::vector<float> sdf;
+    std::vector<uint16_t> sdf;   // d2 per voxel
 };
 
 bool load(const char* path, const char* sdf_path, Problem& p)
@@ -87,7 +87,7 @@ bool load(const char* path, const char* sdf_path, Problem& p)
     if (!f) return false;
     p.sdf.resize((size_t)n * n * n);
     std::ifstream b(sdf_path, std::ios::binary);
-    b.read(reinterpret_cast<char*>(p.sdf.data()), p.sdf.size() * sizeof(float));
+    b.read(reinterpret_cast<char*>(p.sdf.data()), p.sdf.size() * sizeof(uint16_t));
     if (!b) return false;
     g.data = p.sdf.data();
     g.data_on_device = 0;

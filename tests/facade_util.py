@@ -40,7 +40,7 @@ def write_problem(p, directory):
     with open(prob, "w") as f:
         f.write("\n".join(rows) + "\n")
     sdf = os.path.join(directory, "sdf.bin")
-    np.ascontiguousarray(p.sdf, np.float32).tofile(sdf)
+    np.ascontiguousarray(p.sdf, np.uint16).tofile(sdf)
     return prob, sdf
 
 

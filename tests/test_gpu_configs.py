@@ -38,9 +38,9 @@ def problem_on_device_sdf(**kw):
     """make_problem without the numpy SDF; the field is built on the device and copied back."""
     p = pb.make_problem(build_grid=False, **kw)
     n = p.grid.n
-    buf = eng.DeviceBuffer(4 * n ** 3)
+    buf = eng.DeviceBuffer(2 * n ** 3)
     eng.sdf_build_device(p, buf.ptr)
-    p.sdf = buf.to_numpy(np.float32, (n, n, n))
+    p.sdf = buf.to_numpy(np.uint16, (n, n, n))
     return p, buf
 
 

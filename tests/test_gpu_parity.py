@@ -245,14 +245,14 @@ def test_run_chunks_match_iterate():
 def test_sdf_build_device_bitwise():
     for n in (32, 64, 96):
         p = make(grid_n=n)
-        buf = eng.DeviceBuffer(4 * n ** 3)
+        buf = eng.DeviceBuffer(2 * n ** 3)
         eng.sdf_build_device(p, buf.ptr)
-        np.testing.assert_array_equal(buf.to_numpy(np.float32, (n, n, n)), p.sdf)
+        np.testing.assert_array_equal(buf.to_numpy(np.uint16, (n, n, n)), p.sdf)
 
 
 def test_engine_on_device_sdf():
     p = make(grid_n=64)
-    buf = eng.DeviceBuffer(4 * 64 ** 3)
+    buf = eng.DeviceBuffer(2 * 64 ** 3)
     eng.sdf_build_device(p, buf.ptr)
     e = eng.Engine(p, sdf_device_ptr=buf.ptr)
     o = po.Oracle(p)
