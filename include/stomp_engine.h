@@ -227,12 +227,16 @@ int stomp_engine_get_best_torques(stomp_engine* e, double* torques);
  *                       (J x N; row 0 of the reference's per-joint update matrices), theta untouched
  *   add_extra_rollouts  addExtraRollouts (:443-462) of num = 1 rollout: parameters J x N and its
  *                       state costs N; noise against the current theta
+ *   reset               setNumRollouts (:96-147) with the engine's own counts: the reuse state
+ *                       starts over (the next iteration generates every rollout, a pending extra
+ *                       rollout is dropped from the next ranking)
  * Applying the update is Policy::updateParameters: stomp_engine_get_theta / set_theta. */
 int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* noise_stddev, double* rollouts,
                           int32_t* num_generated);
 int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double control_cost_weight, double* totals);
 int stomp_pi_improve_policy(stomp_engine* e, double* updates);
 int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* params, const double* costs);
+int stomp_pi_reset(stomp_engine* e);
 int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj);
 int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj);
 

@@ -16,9 +16,10 @@
 //   * the KDL tree / collision points / distance field arrive as plain tables
 //     (StompRobotModel, StompCollisionSpace); orientation path constraints arrive as
 //     Constraints; the ROS publishers are not taken (no visualisation)
-//   * the rollouts, the policy parameters and the PolicyImprovement state live in HBM inside
-//     one engine; PolicyImprovement therefore works on the policy of a StompOptimizer, and
-//     the rollout counts / time steps are fixed when that optimizer (its engine) is created
+//   * when the policy is a StompOptimizer's, the rollouts, the policy parameters and the
+//     PolicyImprovement state live in HBM inside its engine (the counts fixed when the engine is
+//     created); any other Policy, or rollout counts other than the engine's (setNumRollouts),
+//     runs PolicyImprovement on the host with the same arithmetic and noise stream
 // Failures return false and leave the reason in lastError() (the reference logs with
 // ROS_ERROR and returns false).  One optimizer owns one engine (one HIP device stream).
 #ifndef STOMP_MOTION_PLANNER_STOMP_FACADE_H
@@ -245,14 +246,26 @@ private:
     std::string error_;
 };
 
-// policy_improvement.h:65-126 / policy_improvement.cpp:64-489 over the engine's rollout set
-// (stomp_pi_* of the C ABI).  The policy must be the CovariantTrajectoryPolicy of a
-// StompOptimizer: its rollouts, noise generators and projection matrices live in that engine.
+// policy_improvement.h:65-126 / policy_improvement.cpp:64-489.  Two places the rollout set can
+// live, with the same results:
+//   * the engine of a StompOptimizer (stomp_pi_* of the C ABI) when the policy is that optimizer's
+//     CovariantTrajectoryPolicy and the counts are the engine's;
+//   * the host, for any other Policy, or after setNumRollouts asks for counts the engine was not
+//     created with: the reference's algorithm over the Policy interface (getControlCosts ->
+//     R^-1, chol, projection; computeControlCosts; getParameters), with the engine's noise stream
+//     (Philox normals keyed by seed, iteration, dimension, rollout) and arithmetic contract (fma
+//     chains for L z and M eps, 64-rollout blocked sums, deterministic exp).
+// The policy's num_parameters must equal num_time_steps in every dimension (identity basis, as
+// computeParameterUpdates' noise .* probabilities requires).
 class PolicyImprovement {
 public:
+    PolicyImprovement();
+    ~PolicyImprovement();
     bool initialize(const int num_rollouts, const int num_time_steps, const int num_reused_rollouts,
                     const int num_extra_rollouts, std::shared_ptr<Policy> policy, bool use_cumulative_costs = true);
-    // the counts are fixed when the engine is created: accepted when they match it
+    // policy_improvement.cpp:96-147: new counts, the reuse state reset (the next getRollouts
+    // generates every rollout); counts the engine was not created with move the rollout set to
+    // the host
     bool setNumRollouts(const int num_rollouts, const int num_reused_rollouts, const int num_extra_rollouts);
     // the K_gen new rollouts [K_gen][J] N; noise_stddev per joint
     bool getRollouts(std::vector<std::vector<VectorXd>>& rollouts, const std::vector<double>& noise_stddev);
@@ -266,14 +279,24 @@ public:
     // reference's generators are stateful); each getRollouts uses the current key and advances
     // it by one, starting at 1.  PolicyImprovementLoop sets it to runSingleIteration's number.
     void setNoiseIteration(int iteration) { noise_iteration_ = iteration; }
+    // the noise key of the host rollout set (the engine's comes from StompParameters::seed;
+    // a StompOptimizer's policy sets it from there)
+    void setNoiseSeed(uint64_t seed) { seed_ = seed; }
+    // true while the rollout set lives in a StompOptimizer's engine
+    bool onEngine() const { return engine_ != nullptr && !host_; }
     const std::string& lastError() const { return error_; }
 
 private:
+    struct HostRollouts;
     bool check(int rc);
+    bool hostInitialize(int num_rollouts, int num_reused_rollouts, int num_extra_rollouts);
     std::shared_ptr<Policy> policy_;
     StompOptimizer* owner_ = nullptr;
     stomp_engine* engine_ = nullptr;
+    std::shared_ptr<HostRollouts> host_;
+    uint64_t seed_ = 0x53544F4D50000000ull;
     int J_ = 0, N_ = 0, K_ = 0, K_gen_ = 0, noise_iteration_ = 1;
+    bool use_cumulative_ = false;
     bool initialized_ = false;
     std::string error_;
 };
@@ -283,11 +306,13 @@ private:
 // as the reference does.  When the task is a StompOptimizer the whole iteration runs as the
 // engine's fused launch sequence instead (stomp_engine_iterate, bit-identical results), unless
 // setUseFusedIteration(false).  The loop parameters (rollout counts, noise schedule) are the
-// ones of the StompOptimizer that owns the task's policy (the reference reads the same
+// ones of the StompOptimizer that owns the task's policy, or, for a task whose policy is not a
+// StompOptimizer's, the StompParameters given to initialize (the reference reads the same
 // params.yaml values from the node handle, policy_improvement_loop.cpp:112-123).
 class PolicyImprovementLoop {
 public:
     bool initialize(std::shared_ptr<Task> task);
+    bool initialize(std::shared_ptr<Task> task, const StompParameters& parameters);
     bool runSingleIteration(int iteration_number);
     void setUseFusedIteration(bool on) { fused_ = on; }
     const std::string& lastError() const { return error_; }

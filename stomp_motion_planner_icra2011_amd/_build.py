@@ -87,9 +87,14 @@ FACADE_HDR = os.path.join(INCLUDE, "stomp_motion_planner", "stomp_facade.h")
 def build_facade(verbose: bool = False, force: bool = False) -> str:
     """libstomp_facade.so: the reference-shaped C++ classes over the C ABI (host code only)."""
     lib = build(verbose=verbose)
-    deps = [FACADE_SRC, FACADE_HDR, os.path.join(INCLUDE, "stomp_engine.h"), lib]
+    # the host PolicyImprovement shares the engine's setup (R^-1, chol, projection) and noise
+    # (stomp_math.h) code: compiled in, with the engine's one-rounding-per-operation contract
+    setup = os.path.join(CSRC, "setup.cpp")
+    deps = [FACADE_SRC, FACADE_HDR, os.path.join(INCLUDE, "stomp_engine.h"), lib, setup,
+            os.path.join(CSRC, "setup.h"), os.path.join(CSRC, "stomp_math.h")]
     if force or _newer(FACADE_LIB, deps):
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + INCLUDE, FACADE_SRC, "-o", FACADE_LIB,
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-ffp-contract=off", "-fno-fast-math",
+               "-I" + INCLUDE, "-I" + CSRC, FACADE_SRC, setup, "-o", FACADE_LIB,
                "-L" + PKG, "-l:libstomp_engine.so", "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

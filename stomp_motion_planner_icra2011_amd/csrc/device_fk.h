@@ -126,16 +126,22 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // one value where floor(u + 0.5) != round(u) for u >= 0, u = 0.5 - 2^-54, is below 0.5 and
 // rejected by the range test).  So the range test moves onto u and each axis costs sub, mul,
 // two compares, add and floor.
-// Returns the voxel's squared cell distance d2 (0 outside: distance 0).
-__device__ __forceinline__ unsigned sdf_d2(const DevModel& m, const double* __restrict__ p)
+// The voxel index of p (cell 0 when p reads distance 0: ok = false).
+__device__ __forceinline__ unsigned sdf_cell(const DevModel& m, const double* __restrict__ p, bool& ok)
 {
     const double ux = (p[0] - m.ox) * m.inv_res;
     const double uy = (p[1] - m.oy) * m.inv_res;
     const double uz = (p[2] - m.oz) * m.inv_res;
-    const bool ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
+    ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
     const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
-    const unsigned idx = (unsigned)(ok ? cell : 0.0);
-    const unsigned v = m.sdf[idx];
+    return (unsigned)(ok ? cell : 0.0);
+}
+
+// Returns the voxel's squared cell distance d2 (0 outside: distance 0).
+__device__ __forceinline__ unsigned sdf_d2(const DevModel& m, const double* __restrict__ p)
+{
+    bool ok;
+    const unsigned v = m.sdf[sdf_cell(m, p, ok)];
     return ok ? v : 0u;
 }
 

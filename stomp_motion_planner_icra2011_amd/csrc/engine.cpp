@@ -718,6 +718,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         if (pre && e->pre_host == 1) {
             ca.pre_rows = e->K_loc;
             ca.pre_next = pregen_args(e, it + 1);
+            ca.ctl_by_pre = ca.pre_rows >= ca.num_noisy ? 1 : 0;
             e->pre_it = it + 1;
         }
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
@@ -1663,6 +1664,18 @@ int stomp_pi_improve_policy(stomp_engine* e, double* updates)
     return 0;
 }
 
+// setNumRollouts with the engine's counts (policy_improvement.cpp:139-141): rollouts_reused_next_
+// and extra_rollouts_added_ cleared
+int stomp_pi_reset(stomp_engine* e)
+{
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    DeviceGuard dg(e->device);
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->reused_next = false;
+    e->extra_added = false;
+    return 0;
+}
+
 int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* params, const double* costs)
 {
     if (!e || !params || !costs) return fail(e, STOMP_E_INVALID, "null argument");
@@ -2278,6 +2291,7 @@ int stomp_group_run(stomp_group* g, int32_t first, int32_t count)
             ca.member = member; ca.state_out = e->d_state;
             ca.pre_rows = e->K_loc;
             ca.pre_next = pregen_args(e, it + 1);
+            ca.ctl_by_pre = 1;
             e->pre_it = it + 1;
             if (e->pending_member >= 0) {
                 ca.x_params = e->d_theta; ca.x_member = e->pending_member;

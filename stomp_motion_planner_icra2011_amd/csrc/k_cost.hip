@@ -130,6 +130,11 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double* pA = (double*)(lds_raw + L.nzA);
             double* pB = (double*)(lds_raw + L.nzB);
             const int r = bid - nro;
+            if (!PHASED && a.ctl_by_pre && r < a.num_noisy && !(a.stop && *a.stop)) {
+                // this iteration's row r priced here instead of on its rollout's critical path
+                pre_row_control<BLOCK>(a.nz, r, pA, pB, threadIdx.x);
+                __syncthreads();   // pA / pB are the normals' buffers next
+            }
             rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
             if (J <= 8) {
                 pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
@@ -217,7 +222,9 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         if (defer) rollout_project<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
         else rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
     } else if (pre) {
-        if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
+        // the control costs are left to the pregen block of this row (ctl_by_pre) or, in the
+        // phased body, to the FK-idle waves (defer)
+        if (defer || (!PHASED && a.ctl_by_pre)) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
         else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid, pc0);
     }
     if (tid == 0) flag = 0;
@@ -517,25 +524,41 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         const int ns = se - sb;
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
         // flight) and serves spheres g, g + G, ... of the slot
-        if (pg < G) {
-            // every sphere of the run this lane takes (at most kLaneSpheres: a run holds <= 16
-            // spheres and G >= 2 when N <= 128; <= 8 spheres and G >= 1 otherwise) is looked up
-            // with all its gathers in flight at once; the potentials and the pair list follow
+        // Every sphere of the run this lane takes (at most kLaneSpheres: a run holds <= 16
+        // spheres and G >= 2 when N <= 128; <= 8 spheres and G >= 1 otherwise) is looked up with
+        // all its gathers in flight at once, and they stay in flight through the FK advance
+        // below: no branch around the loads (every lane runs them; past the run's spheres, and
+        // on the lanes past the pair lanes, a lookup repeats a valid one and is not used) and the
+        // out-of-grid select at the use, since the compiler waits for a load whose register
+        // leaves a divergent region or is copied
+        unsigned dv[kLaneSpheres];
+        unsigned okm = 0;
+        {
             double F[12];
 #pragma unroll
             for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
-            unsigned dv[kLaneSpheres];
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
-                if (u * G >= ns) break;   // uniform
                 const double* pos = sph[sb + min(pg + u * G, ns - 1)].pos;
                 double x[3];
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
                     x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
-                dv[u] = sdf_d2(m, x);
+                bool ok;
+                const unsigned idx = sdf_cell(m, x, ok);
+                dv[u] = m.sdf[idx];
+                okm |= (unsigned)ok << u;
             }
-            STAMP(40 + run);
+        }
+        STAMP(40 + run);
+        // while the gathers are in flight the FK lanes run the program on to the next sphere
+        // segment (C in registers; fb keeps this slot's frame for the velocities, and the next
+        // frame is published after the fold)
+        __builtin_amdgcn_s_setprio(3);
+        const int next_op = fk_advance(op + 1);
+        __builtin_amdgcn_s_setprio(2);
+        if (pg < G) {
+            // the potentials and the pair list
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform
@@ -544,7 +567,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 bool nz = false;
                 if (in) {
                     const DevSphere& sp = sph[sb + q];
-                    const int d2 = (int)dv[u];
+                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
                     col |= d2 < sp.col_lim;
                     nz = d2 < sp.zero_lim;
                     // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
@@ -574,13 +597,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
             av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
         }
-        // C is reloaded from fb (not kept live across the pairs)
-        if (fk_lane) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
-        }
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
         __builtin_amdgcn_s_setprio(3);
@@ -599,8 +615,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 }
             }
         }
-        // the program's control flow is uniform, so every lane arrives at the same next op
-        op = fk_advance(op + 1);
+        // the program's control flow is uniform, so every lane has the same next op
+        op = next_op;
         __builtin_amdgcn_s_setprio(2);
         STAMP(13 + 4 * run);
         ++run;

@@ -189,6 +189,9 @@ struct CostArgs {
     int x_member;
     int pre_rows;               // > 0: blocks after the rollouts make k_pregen's rows of pre_next (the
     NoiseArgs pre_next;         // next iteration) at low priority in the same dispatch
+    int ctl_by_pre;             // with fused_noise 2 and pre_rows >= num_noisy: pregen block r also prices
+                                // this iteration's row r (computeControlCosts, off the rollout's
+                                // critical path); the rollout workgroups skip it
     double* x_state;
     uint8_t* x_cf;
     double* x_traj;

@@ -578,6 +578,30 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
     if (!DEFER) rollout_control<BLOCK>(a, row, xs, zB, tid);
 }
 
+// computeControlCosts of row r from k_pregen's eps and M eps (covariant_trajectory_policy.cpp:
+// 228-255 via policy_improvement.cpp:292-299): x = (theta + eps) + M eps, the expressions of
+// rollout_from_pre, then rollout_control into a.control.  Run by the rollout launch's pregen block
+// r, so the rollout workgroup of row r leaves the pricing out of its critical path.
+template <int BLOCK>
+__device__ __forceinline__ void pre_row_control(const NoiseArgs& a, int r, double* xs, double* cs, int tid)
+{
+    const int J = a.J, N = a.N, Nall = a.Nall, JN = J * N;
+    for (int idx0 = 0; idx0 < JN; idx0 += 4 * BLOCK) {
+        PreChunk c;
+        pre_chunk_load<BLOCK>(a, r, idx0, tid, c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = idx0 + tid + u * BLOCK;
+            if (idx < JN) {
+                const int d = idx / N, i = idx - d * N;
+                const double p = c.th[u] + c.e[u];
+                xs[d * Nall + i + 6] = p + c.mp[u];
+            }
+        }
+    }
+    rollout_control<BLOCK>(a, (size_t)r * JN, xs, cs, tid, nullptr);
+}
+
 // the engine runs the fused phase for J <= 16 (at most four groups of 4 joint columns)
 template <int BLOCK, bool DEFER = false>
 __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,

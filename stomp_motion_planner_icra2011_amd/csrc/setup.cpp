@@ -77,6 +77,22 @@ bool spd_inverse(const std::vector<double>& A, int n, std::vector<double>& X)
 
 }  // namespace
 
+std::string noise_setup(const std::vector<double>& R, int n, std::vector<double>& Rinv, std::vector<double>& L,
+                        std::vector<double>& M)
+{
+    if (n <= 0 || R.size() != (size_t)n * n) return "control cost matrix has the wrong size";
+    if (!spd_inverse(R, n, Rinv) || !cholesky(Rinv, n, L)) return "control cost matrix R is not positive definite";
+    M.assign((size_t)n * n, 0.0);
+    for (int p = 0; p < n; ++p) {
+        double cmax = Rinv[p];
+        for (int p2 = 1; p2 < n; ++p2)
+            if (Rinv[(size_t)p2 * n + p] > cmax) cmax = Rinv[(size_t)p2 * n + p];
+        double sc = 1.0 / ((double)n * cmax);
+        for (int i = 0; i < n; ++i) M[(size_t)i * n + p] = Rinv[(size_t)i * n + p] * sc;
+    }
+    return std::string();
+}
+
 std::string compute_setup(const SetupInput& in, SetupOutput& out)
 {
     const int J = in.J, N = in.N, Nall = N + 2 * kPad;
@@ -102,16 +118,9 @@ std::string compute_setup(const SetupInput& in, SetupOutput& out)
     std::vector<double> Rfree((size_t)N * N);
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < N; ++j) Rfree[(size_t)i * N + j] = out.Rall[(size_t)(i + kPad) * Nall + (j + kPad)];
-    if (!spd_inverse(Rfree, N, out.Rinv) || !cholesky(out.Rinv, N, out.L))
-        return "control cost matrix R is not positive definite";
-
-    out.M.assign((size_t)N * N, 0.0);
-    for (int p = 0; p < N; ++p) {
-        double cmax = out.Rinv[p];
-        for (int p2 = 1; p2 < N; ++p2)
-            if (out.Rinv[(size_t)p2 * N + p] > cmax) cmax = out.Rinv[(size_t)p2 * N + p];
-        double sc = 1.0 / ((double)N * cmax);
-        for (int i = 0; i < N; ++i) out.M[(size_t)i * N + p] = out.Rinv[(size_t)i * N + p] * sc;
+    {
+        std::string msg = noise_setup(Rfree, N, out.Rinv, out.L, out.M);
+        if (!msg.empty()) return msg;
     }
 
     // StompCost: Q = sum_i (w_i * disc^(i+1)) D_i^T D_i + ridge I with raw stencils

@@ -45,4 +45,11 @@ struct SetupOutput {
 // Returns an empty string on success, otherwise the error message.
 std::string compute_setup(const SetupInput& in, SetupOutput& out);
 
+// PolicyImprovement::initialize's per-dimension noise set-up from a control-cost matrix R
+// (n x n, row-major; policy_improvement.cpp:77-86, 421-441): Rinv = R^-1, L = chol(Rinv) (the
+// MultivariateGaussian factor, multivariate_gaussian.h:76-86) and the projection M (Rinv with
+// column p scaled by 1 / (n max_i Rinv(i, p))).  compute_setup uses it for the free block of R.
+std::string noise_setup(const std::vector<double>& R, int n, std::vector<double>& Rinv, std::vector<double>& L,
+                        std::vector<double>& M);
+
 }  // namespace stomp

@@ -89,7 +89,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_device_selftest", "stomp_device_normals", "stomp_device_alloc", "stomp_device_free",
             "stomp_device_copy_to_host", "stomp_device_count", "stomp_diff_rules", "stomp_comm_local_id",
             "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
-            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_sdf_build_objects",
+            "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_pi_reset", "stomp_sdf_build_objects",
             "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
             "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy"]
 
@@ -127,6 +127,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_pi_set_rollout_costs.argtypes = [P, dp, C.c_double, dp]
     l.stomp_pi_improve_policy.argtypes = [P, dp]
     l.stomp_pi_add_extra_rollouts.argtypes = [P, C.c_int32, dp, dp]
+    l.stomp_pi_reset.argtypes = [P]
     l.stomp_engine_get_last_trajectory.argtypes = [P, dp]
     l.stomp_engine_get_rollouts.argtypes = [P, C.c_char_p, dp]
     l.stomp_engine_get_matrix.argtypes = [P, C.c_char_p, C.c_int32, dp]

@@ -2,8 +2,13 @@
 // See include/stomp_motion_planner/stomp_facade.h for the mapping to the reference.
 #include "stomp_motion_planner/stomp_facade.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <utility>
+
+#include "setup.h"
+#include "stomp_math.h"
 
 namespace stomp_motion_planner {
 
@@ -387,6 +392,73 @@ bool CovariantTrajectoryPolicy::computeControlCosts(const std::vector<MatrixXd>&
 
 // ------------------------------------------------------------------ PolicyImprovement
 
+// The host rollout set (policy_improvement.cpp:64-489 for any Policy).  Arithmetic contract as
+// the engine's and the oracle's: L z and M eps as k-ascending fma chains,
+// rollout sums in 64-rollout blocks, the deterministic exp of stomp_math.h, everything else one
+// rounding per operation in the reference's order.
+struct PolicyImprovement::HostRollouts {
+    struct Rollout {
+        std::vector<VectorXd> parameters, noise, noise_projected, control_costs, probabilities;
+        VectorXd state_costs;
+    };
+    int J = 0, N = 0, K = 0, Kr = 0, Kx = 0, K_gen = 0;
+    bool reused_next = false, extra_added = false;
+    std::vector<MatrixXd> R;                       // control_costs_ (policy->getControlCosts)
+    std::vector<std::vector<double>> Rinv, L, M;   // per dimension, N x N row-major
+    std::vector<Rollout> rollouts, extra;
+    std::vector<VectorXd> parameters;              // parameters_ (copyParametersFromPolicy)
+    double control_cost_weight = 0.0;
+
+    Rollout blank() const
+    {
+        Rollout r;
+        r.parameters.assign(J, VectorXd(N, 0.0));
+        r.noise = r.noise_projected = r.control_costs = r.probabilities = r.parameters;
+        r.state_costs.assign(N, 0.0);
+        return r;
+    }
+    // y = A x, k ascending, one rounding per multiply-add; lower: the triangle k <= i only (the
+    // zeros above it add nothing)
+    void fma_product(const std::vector<double>& A, const VectorXd& x, VectorXd& y, bool lower) const
+    {
+        y.assign(N, 0.0);
+        for (int i = 0; i < N; ++i) {
+            double s = 0.0;
+            const int kend = lower ? i + 1 : N;
+            for (int k = 0; k < kend; ++k) s = std::fma(A[(size_t)i * N + k], x[k], s);
+            y[i] = s;
+        }
+    }
+    // Rollout::getCost (policy_improvement.cpp:149-156), sums in index order
+    static double cost(const Rollout& r)
+    {
+        double c = r.state_costs[0];
+        for (size_t t = 1; t < r.state_costs.size(); ++t) c += r.state_costs[t];
+        for (const VectorXd& x : r.control_costs) {
+            double sd = x[0];
+            for (size_t t = 1; t < x.size(); ++t) sd += x[t];
+            c += sd;
+        }
+        return c;
+    }
+    // sum_r v(r) in fixed 64-rollout blocks (the engine's canonical order; sequential for K <= 64)
+    template <class F>
+    double blocked_sum(int n, F v) const
+    {
+        double total = 0.0;
+        for (int b0 = 0; b0 < n; b0 += 64) {
+            double part = 0.0;
+            const int b1 = b0 + 64 < n ? b0 + 64 : n;
+            for (int r = b0; r < b1; ++r) part += v(r);
+            total += part;
+        }
+        return total;
+    }
+};
+
+PolicyImprovement::PolicyImprovement() = default;
+PolicyImprovement::~PolicyImprovement() = default;
+
 bool PolicyImprovement::check(int rc)
 {
     if (rc == 0) return true;
@@ -399,28 +471,74 @@ bool PolicyImprovement::initialize(const int num_rollouts, const int num_time_st
                                    bool use_cumulative_costs)
 {
     initialized_ = false;
-    auto* ctp = dynamic_cast<CovariantTrajectoryPolicy*>(policy.get());
-    if (!ctp || !ctp->owner() || !ctp->owner()->ok()) {
-        error_ = "PolicyImprovement::initialize: the policy must be a StompOptimizer's CovariantTrajectoryPolicy";
+    host_.reset();
+    owner_ = nullptr;
+    engine_ = nullptr;
+    if (!policy) {
+        error_ = "PolicyImprovement::initialize: null policy";
         return false;
     }
-    owner_ = ctp->owner();
-    engine_ = owner_->engine_;
     policy_ = policy;
-    J_ = owner_->J_;
-    N_ = owner_->N_;
-    K_ = owner_->parameters_->num_rollouts;
-    if (num_time_steps != N_) {
-        error_ = "PolicyImprovement::initialize: num_time_steps differs from the engine's";
-        return false;
-    }
-    if (use_cumulative_costs != owner_->parameters_->use_cumulative_costs) {
-        error_ = "PolicyImprovement::initialize: use_cumulative_costs differs from the engine's";
-        return false;
+    N_ = num_time_steps;
+    use_cumulative_ = use_cumulative_costs;
+    noise_iteration_ = 1;
+    auto* ctp = dynamic_cast<CovariantTrajectoryPolicy*>(policy.get());
+    if (ctp && ctp->owner() && ctp->owner()->ok()) {
+        owner_ = ctp->owner();
+        engine_ = owner_->engine_;
+        J_ = owner_->J_;
+        K_ = owner_->parameters_->num_rollouts;
+        seed_ = owner_->parameters_->seed;
+        if (num_time_steps != owner_->N_) {
+            error_ = "PolicyImprovement::initialize: num_time_steps differs from the engine's";
+            return false;
+        }
+        if (use_cumulative_costs != owner_->parameters_->use_cumulative_costs) {
+            // the engine's setting is fixed at creation: the rollout set moves to the host
+            if (!hostInitialize(num_rollouts, num_reused_rollouts, num_extra_rollouts)) return false;
+            return (initialized_ = true);
+        }
     }
     if (!setNumRollouts(num_rollouts, num_reused_rollouts, num_extra_rollouts)) return false;
-    noise_iteration_ = 1;
     return (initialized_ = true);
+}
+
+// PolicyImprovement::initialize (policy_improvement.cpp:64-94) with the rollout set on the host
+bool PolicyImprovement::hostInitialize(int num_rollouts, int num_reused_rollouts, int num_extra_rollouts)
+{
+    auto h = std::make_shared<HostRollouts>();
+    int J = 0;
+    std::vector<int> np;
+    if (!policy_->setNumTimeSteps(N_) || !policy_->getControlCosts(h->R) || !policy_->getNumDimensions(J) ||
+        !policy_->getNumParameters(np) || !policy_->getParameters(h->parameters)) {
+        error_ = "PolicyImprovement::initialize: policy query failed";
+        return false;
+    }
+    if (J <= 0 || (int)np.size() != J || (int)h->R.size() != J || (int)h->parameters.size() != J) {
+        error_ = "PolicyImprovement::initialize: policy dimensions disagree";
+        return false;
+    }
+    for (int d = 0; d < J; ++d)
+        if (np[d] != N_ || h->R[d].rows() != N_ || h->R[d].cols() != N_ || (int)h->parameters[d].size() != N_) {
+            error_ = "PolicyImprovement::initialize: num_parameters must equal num_time_steps (identity basis)";
+            return false;
+        }
+    h->J = J;
+    h->N = N_;
+    h->Rinv.resize(J);
+    h->L.resize(J);
+    h->M.resize(J);
+    for (int d = 0; d < J; ++d) {
+        // inv_control_costs_, MultivariateGaussian(0, R^-1), preComputeProjectionMatrices
+        std::string msg = stomp::noise_setup(h->R[d].data_, N_, h->Rinv[d], h->L[d], h->M[d]);
+        if (!msg.empty()) {
+            error_ = "PolicyImprovement::initialize: " + msg;
+            return false;
+        }
+    }
+    J_ = J;
+    host_ = h;
+    return setNumRollouts(num_rollouts, num_reused_rollouts, num_extra_rollouts);
 }
 
 bool PolicyImprovement::setNumRollouts(const int num_rollouts, const int num_reused_rollouts,
@@ -430,11 +548,29 @@ bool PolicyImprovement::setNumRollouts(const int num_rollouts, const int num_reu
         error_ = "Number of reused rollouts must be strictly less than number of rollouts.";
         return false;
     }
-    if (!owner_ || num_rollouts != K_ || num_reused_rollouts != owner_->parameters_->num_reused_rollouts ||
-        num_extra_rollouts != 1) {
-        error_ = "setNumRollouts: the engine's rollout counts are fixed at creation (and one extra rollout)";
+    if (num_rollouts <= 0 || num_reused_rollouts < 0 || num_extra_rollouts < 0) {
+        error_ = "setNumRollouts: negative or zero rollout count";
         return false;
     }
+    if (!host_) {
+        if (owner_ && num_rollouts == owner_->parameters_->num_rollouts &&
+            num_reused_rollouts == owner_->parameters_->num_reused_rollouts && num_extra_rollouts == 1) {
+            // the engine's own counts: its reuse state starts over on the next getRollouts
+            K_ = num_rollouts;
+            return engine_ ? check(stomp_pi_reset(engine_)) : true;
+        }
+        return hostInitialize(num_rollouts, num_reused_rollouts, num_extra_rollouts);
+    }
+    HostRollouts& h = *host_;
+    h.K = num_rollouts;
+    h.Kr = num_reused_rollouts;
+    h.Kx = num_extra_rollouts;
+    h.K_gen = 0;
+    h.rollouts.assign(h.K, h.blank());
+    h.extra.assign(h.Kx, h.blank());
+    h.reused_next = false;
+    h.extra_added = false;
+    K_ = h.K;
     return true;
 }
 
@@ -443,15 +579,72 @@ bool PolicyImprovement::getRollouts(std::vector<std::vector<VectorXd>>& rollouts
 {
     if (!initialized_) { error_ = "getRollouts: not initialized"; return false; }
     if ((int)noise_stddev.size() != J_) { error_ = "getRollouts: one noise_stddev per dimension"; return false; }
-    std::vector<double> buf((size_t)K_ * J_ * N_);
-    int32_t n = 0;
-    if (!check(stomp_pi_get_rollouts(engine_, noise_iteration_, noise_stddev.data(), buf.data(), &n))) return false;
+    if (!host_) {
+        std::vector<double> buf((size_t)K_ * J_ * N_);
+        int32_t n = 0;
+        if (!check(stomp_pi_get_rollouts(engine_, noise_iteration_, noise_stddev.data(), buf.data(), &n))) return false;
+        ++noise_iteration_;
+        K_gen_ = n;
+        rollouts.assign(n, std::vector<VectorXd>(J_, VectorXd(N_)));
+        for (int r = 0; r < n; ++r)
+            for (int d = 0; d < J_; ++d)
+                for (int t = 0; t < N_; ++t) rollouts[r][d][t] = buf[((size_t)r * J_ + d) * N_ + t];
+        return true;
+    }
+    // generateRollouts (policy_improvement.cpp:158-239)
+    HostRollouts& h = *host_;
+    if (!policy_->getParameters(h.parameters)) { error_ = "getRollouts: policy getParameters failed"; return false; }
+    h.K_gen = h.K - h.Kr;
+    if (!h.reused_next) {
+        h.K_gen = h.K;
+        if (h.Kr > 0) h.reused_next = true;
+    } else {
+        // the best K_r of the previous rollouts and the extra rollouts, by (cost, index): the
+        // extra ones carry the negative indices -r-1, as the reference's sorter
+        std::vector<std::pair<double, int>> sorter;
+        for (int r = 0; r < h.K; ++r) sorter.push_back({HostRollouts::cost(h.rollouts[r]), r});
+        if (h.extra_added) {
+            for (int r = 0; r < h.Kx; ++r) sorter.push_back({HostRollouts::cost(h.extra[r]), -r - 1});
+            h.extra_added = false;
+        }
+        std::sort(sorter.begin(), sorter.end());
+        std::vector<HostRollouts::Rollout> reused;
+        for (int r = 0; r < h.Kr; ++r) {
+            const int idx = sorter[r].second;
+            reused.push_back(idx >= 0 ? h.rollouts[idx] : h.extra[-idx - 1]);
+        }
+        for (int r = 0; r < h.Kr; ++r) {
+            HostRollouts::Rollout& dst = h.rollouts[h.K_gen + r];
+            dst = reused[r];
+            for (int d = 0; d < h.J; ++d)
+                for (int t = 0; t < h.N; ++t) dst.noise[d][t] = dst.parameters[d][t] - h.parameters[d][t];
+        }
+    }
+    // new rollouts: eps = sigma_d * (0 + L z), z the counter-based normals of (seed, iteration,
+    // dimension, rollout); parameters = theta + eps
+    VectorXd z(h.N), lz;
+    for (int d = 0; d < h.J; ++d)
+        for (int r = 0; r < h.K_gen; ++r) {
+            for (int p = 0; 2 * p < h.N; ++p) {
+                double z0, z1;
+                stomp::normal_pair(seed_, noise_iteration_, d, r, p, &z0, &z1);
+                z[2 * p] = z0;
+                if (2 * p + 1 < h.N) z[2 * p + 1] = z1;
+            }
+            h.fma_product(h.L[d], z, lz, true);
+            HostRollouts::Rollout& ro = h.rollouts[r];
+            for (int t = 0; t < h.N; ++t) {
+                ro.noise[d][t] = noise_stddev[d] * (0.0 + lz[t]);
+                ro.parameters[d][t] = h.parameters[d][t] + ro.noise[d][t];
+            }
+        }
     ++noise_iteration_;
-    K_gen_ = n;
-    rollouts.assign(n, std::vector<VectorXd>(J_, VectorXd(N_)));
-    for (int r = 0; r < n; ++r)
-        for (int d = 0; d < J_; ++d)
-            for (int t = 0; t < N_; ++t) rollouts[r][d][t] = buf[((size_t)r * J_ + d) * N_ + t];
+    K_gen_ = h.K_gen;
+    rollouts.clear();
+    for (int r = 0; r < h.K_gen; ++r) rollouts.push_back(h.rollouts[r].parameters);
+    // computeProjectedNoise for every rollout (:283-290, 473-482)
+    for (HostRollouts::Rollout& ro : h.rollouts)
+        for (int d = 0; d < h.J; ++d) h.fma_product(h.M[d], ro.noise[d], ro.noise_projected[d], false);
     return true;
 }
 
@@ -463,21 +656,79 @@ bool PolicyImprovement::setRolloutCosts(const MatrixXd& costs, const double cont
         error_ = "setRolloutCosts: costs must be num_rollouts x num_time_steps";
         return false;
     }
-    std::vector<double> c((size_t)K_ * N_, 0.0);
-    for (int r = 0; r < K_gen_; ++r)
-        for (int t = 0; t < N_; ++t) c[(size_t)r * N_ + t] = costs(r, t);
-    rollout_costs_total.assign(K_, 0.0);
-    return check(stomp_pi_set_rollout_costs(engine_, c.data(), control_cost_weight, rollout_costs_total.data()));
+    if (!host_) {
+        std::vector<double> c((size_t)K_ * N_, 0.0);
+        for (int r = 0; r < K_gen_; ++r)
+            for (int t = 0; t < N_; ++t) c[(size_t)r * N_ + t] = costs(r, t);
+        rollout_costs_total.assign(K_, 0.0);
+        return check(stomp_pi_set_rollout_costs(engine_, c.data(), control_cost_weight, rollout_costs_total.data()));
+    }
+    // :262-281: the control costs of every rollout (computeRolloutControlCosts, :484-489), then
+    // the state costs of the new ones
+    HostRollouts& h = *host_;
+    h.control_cost_weight = control_cost_weight;
+    for (HostRollouts::Rollout& ro : h.rollouts)
+        if (!policy_->computeControlCosts(h.R, ro.parameters, ro.noise_projected, 0.5 * h.control_cost_weight,
+                                          ro.control_costs)) {
+            error_ = "setRolloutCosts: policy computeControlCosts failed";
+            return false;
+        }
+    for (int r = 0; r < h.K_gen; ++r)
+        for (int t = 0; t < h.N; ++t) h.rollouts[r].state_costs[t] = costs(r, t);
+    rollout_costs_total.resize(h.K);
+    for (int r = 0; r < h.K; ++r) rollout_costs_total[r] = HostRollouts::cost(h.rollouts[r]);
+    return true;
 }
 
 bool PolicyImprovement::improvePolicy(std::vector<MatrixXd>& parameter_updates)
 {
     if (!initialized_) { error_ = "improvePolicy: not initialized"; return false; }
-    std::vector<double> u((size_t)J_ * N_);
-    if (!check(stomp_pi_improve_policy(engine_, u.data()))) return false;
-    parameter_updates.assign(J_, MatrixXd(N_, N_));
-    for (int d = 0; d < J_; ++d)
-        for (int t = 0; t < N_; ++t) parameter_updates[d](0, t) = u[(size_t)d * N_ + t];
+    if (!host_) {
+        std::vector<double> u((size_t)J_ * N_);
+        if (!check(stomp_pi_improve_policy(engine_, u.data()))) return false;
+        parameter_updates.assign(J_, MatrixXd(N_, N_));
+        for (int d = 0; d < J_; ++d)
+            for (int t = 0; t < N_; ++t) parameter_updates[d](0, t) = u[(size_t)d * N_ + t];
+        return true;
+    }
+    // :385-401: cumulative costs (:301-320), probabilities (:322-368), updates (:370-383)
+    HostRollouts& h = *host_;
+    const int K = h.K, N = h.N;
+    parameter_updates.assign(h.J, MatrixXd(N, N));
+    std::vector<double> cum((size_t)K * N);
+    VectorXd upd(N), delta;
+    for (int d = 0; d < h.J; ++d) {
+        for (int r = 0; r < K; ++r) {
+            double* c = cum.data() + (size_t)r * N;
+            for (int t = 0; t < N; ++t) c[t] = h.rollouts[r].state_costs[t] + h.rollouts[r].control_costs[d][t];
+            if (use_cumulative_)
+                for (int t = N - 2; t >= 0; --t) c[t] += c[t + 1];
+        }
+        for (int t = 0; t < N; ++t) {
+            double mn = cum[t], mx = mn;
+            for (int r = 1; r < K; ++r) {
+                const double c = cum[(size_t)r * N + t];
+                if (c < mn) mn = c;
+                if (c > mx) mx = c;
+            }
+            double denom = mx - mn;
+            if (denom < 1e-8) denom = 1e-8;
+            for (int r = 0; r < K; ++r)
+                h.rollouts[r].probabilities[d][t] = stomp::det_exp(-10.0 * (cum[(size_t)r * N + t] - mn) / denom);
+            const double psum = h.blocked_sum(K, [&](int r) { return h.rollouts[r].probabilities[d][t]; });
+            for (int r = 0; r < K; ++r) h.rollouts[r].probabilities[d][t] /= psum;
+            upd[t] = h.blocked_sum(
+                K, [&](int r) { return h.rollouts[r].noise[d][t] * h.rollouts[r].probabilities[d][t]; });
+        }
+        // projection_matrix_[d] * the row (dense, k ascending, one rounding per operation)
+        delta.assign(N, 0.0);
+        for (int i = 0; i < N; ++i) {
+            double s = 0.0;
+            for (int k = 0; k < N; ++k) s += h.M[d][(size_t)i * N + k] * upd[k];
+            delta[i] = s;
+        }
+        for (int t = 0; t < N; ++t) parameter_updates[d](0, t) = delta[t];
+    }
     return true;
 }
 
@@ -485,17 +736,47 @@ bool PolicyImprovement::addExtraRollouts(std::vector<std::vector<VectorXd>>& rol
                                          std::vector<VectorXd>& rollout_costs)
 {
     if (!initialized_) { error_ = "addExtraRollouts: not initialized"; return false; }
-    if (rollouts.size() != 1 || rollout_costs.size() != 1 || (int)rollouts[0].size() != J_ ||
-        (int)rollout_costs[0].size() != N_) {
-        error_ = "addExtraRollouts: one extra rollout ([J] N parameters, N costs)";
+    if (!host_) {
+        if (rollouts.size() != 1 || rollout_costs.size() != 1 || (int)rollouts[0].size() != J_ ||
+            (int)rollout_costs[0].size() != N_) {
+            error_ = "addExtraRollouts: one extra rollout ([J] N parameters, N costs)";
+            return false;
+        }
+        std::vector<double> prm((size_t)J_ * N_);
+        for (int d = 0; d < J_; ++d) {
+            if ((int)rollouts[0][d].size() != N_) { error_ = "addExtraRollouts: bad parameter size"; return false; }
+            for (int t = 0; t < N_; ++t) prm[(size_t)d * N_ + t] = rollouts[0][d][t];
+        }
+        return check(stomp_pi_add_extra_rollouts(engine_, 1, prm.data(), rollout_costs[0].data()));
+    }
+    // :443-489: noise = parameters - theta, its projection and control costs
+    HostRollouts& h = *host_;
+    if ((int)rollouts.size() != h.Kx || (int)rollout_costs.size() != h.Kx) {
+        error_ = "addExtraRollouts: num_extra_rollouts rollouts and costs";
         return false;
     }
-    std::vector<double> prm((size_t)J_ * N_);
-    for (int d = 0; d < J_; ++d) {
-        if ((int)rollouts[0][d].size() != N_) { error_ = "addExtraRollouts: bad parameter size"; return false; }
-        for (int t = 0; t < N_; ++t) prm[(size_t)d * N_ + t] = rollouts[0][d][t];
+    if (!policy_->getParameters(h.parameters)) { error_ = "addExtraRollouts: policy getParameters failed"; return false; }
+    for (int r = 0; r < h.Kx; ++r) {
+        if ((int)rollouts[r].size() != h.J || (int)rollout_costs[r].size() != h.N) {
+            error_ = "addExtraRollouts: bad rollout size";
+            return false;
+        }
+        HostRollouts::Rollout& ro = h.extra[r];
+        ro.parameters = rollouts[r];
+        ro.state_costs = rollout_costs[r];
+        for (int d = 0; d < h.J; ++d) {
+            if ((int)ro.parameters[d].size() != h.N) { error_ = "addExtraRollouts: bad parameter size"; return false; }
+            for (int t = 0; t < h.N; ++t) ro.noise[d][t] = ro.parameters[d][t] - h.parameters[d][t];
+            h.fma_product(h.M[d], ro.noise[d], ro.noise_projected[d], false);
+        }
+        if (!policy_->computeControlCosts(h.R, ro.parameters, ro.noise_projected, 0.5 * h.control_cost_weight,
+                                          ro.control_costs)) {
+            error_ = "addExtraRollouts: policy computeControlCosts failed";
+            return false;
+        }
     }
-    return check(stomp_pi_add_extra_rollouts(engine_, 1, prm.data(), rollout_costs[0].data()));
+    h.extra_added = true;
+    return true;
 }
 
 // ------------------------------------------------------------------ PolicyImprovementLoop
@@ -514,18 +795,38 @@ bool PolicyImprovementLoop::initialize(std::shared_ptr<Task> task)
     }
     auto* ctp = dynamic_cast<CovariantTrajectoryPolicy*>(policy.get());
     if (!ctp || !ctp->owner() || !ctp->owner()->ok()) {
-        error_ = "PolicyImprovementLoop::initialize: the task's policy must be a StompOptimizer's "
-                 "CovariantTrajectoryPolicy";
+        error_ = "PolicyImprovementLoop::initialize: a task whose policy is not a StompOptimizer's needs the "
+                 "StompParameters (initialize(task, parameters))";
         return false;
     }
-    owner_ = ctp->owner();
+    return initialize(task, *ctp->owner()->parameters_);
+}
+
+bool PolicyImprovementLoop::initialize(std::shared_ptr<Task> task, const StompParameters& p)
+{
+    optimizer_ = owner_ = nullptr;
+    if (!task) {
+        error_ = "PolicyImprovementLoop::initialize: null task";
+        return false;
+    }
+    std::shared_ptr<Policy> policy;
+    if (!task->getPolicy(policy) || !policy) {
+        error_ = "PolicyImprovementLoop::initialize: the task has no policy";
+        return false;
+    }
+    auto* ctp = dynamic_cast<CovariantTrajectoryPolicy*>(policy.get());
+    if (ctp && ctp->owner() && ctp->owner()->ok()) owner_ = ctp->owner();
     optimizer_ = dynamic_cast<StompOptimizer*>(task.get());
     task_ = task;
     policy_ = policy;
-    // readParameters (policy_improvement_loop.cpp:112-123) from the optimizer's parameters
-    const StompParameters& p = *owner_->parameters_;
+    // readParameters (policy_improvement_loop.cpp:112-123)
     num_rollouts_ = p.num_rollouts;
-    num_time_steps_ = owner_->N_;
+    if (owner_) {
+        num_time_steps_ = owner_->N_;
+    } else if (!policy_->getNumTimeSteps(num_time_steps_)) {
+        error_ = "PolicyImprovementLoop::initialize: policy getNumTimeSteps failed";
+        return false;
+    }
     noise_stddev_ = p.noise_stddev;
     noise_decay_ = p.noise_decay;
     if (!task_->initialize(num_time_steps_) || !task_->getControlCostWeight(control_cost_weight_)) {
@@ -538,6 +839,7 @@ bool PolicyImprovementLoop::initialize(std::shared_ptr<Task> task)
         error_ = "PolicyImprovementLoop::initialize: noise_stddev / noise_decay need one entry per dimension";
         return false;
     }
+    policy_improvement_.setNoiseSeed(p.seed);
     if (!policy_improvement_.initialize(num_rollouts_, num_time_steps_, p.num_reused_rollouts, 1, policy_,
                                         p.use_cumulative_costs)) {
         error_ = policy_improvement_.lastError();
@@ -552,7 +854,8 @@ bool PolicyImprovementLoop::runSingleIteration(int iteration_number)
         error_ = "runSingleIteration: not initialized";
         return false;
     }
-    if (!fused_ || !optimizer_ || optimizer_ != owner_) return runGeneric(iteration_number);
+    if (!fused_ || !optimizer_ || optimizer_ != owner_ || !policy_improvement_.onEngine())
+        return runGeneric(iteration_number);
     // the whole iteration as the engine's fused launch sequence
     stomp_iter_out out{};
     int rc = stomp_engine_iterate(optimizer_->engine_, iteration_number, &out);

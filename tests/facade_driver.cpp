@@ -14,7 +14,15 @@
 //                        does, plus the rollout totals of every setRolloutCosts
 //   mode control_costs : both Policy::computeControlCosts overloads on parameters / noise read
 //                        from in.txt
+//   mode pi_user       : PolicyImprovementLoop over a user Policy (UserPolicy: theta on the host)
+//                        and a user Task (forwarding to the optimizer's execute): the host
+//                        PolicyImprovement path; writes cost and theta per iteration
+//   mode pi_setnum     : pi_steps after setNumRollouts(K, K_r + delta, 1) on the optimizer's policy
+//                        (in.txt: the new K_r): counts the engine was not created with
+//   mode pi_host_cpu   : the host PolicyImprovement with a synthetic policy and task, no device
+//                        (the sanitizer build runs it)
 // The problem file is whitespace-separated text written by tests/facade_util.py.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <fstream>
@@ -120,6 +128,185 @@ private:
     std::shared_ptr<StompOptimizer> o_;
 };
 
+// A user's Policy: CovariantTrajectoryPolicy written against the Policy interface with theta on
+// the host (covariant_trajectory_policy.cpp:168-342): R and the stencil matrices D_i come from the
+// optimizer's policy / engine once, then everything runs here.
+class UserPolicy : public Policy {
+public:
+    UserPolicy(StompOptimizer& opt, const StompTrajectory& tr, const StompParameters& q)
+        : J_(opt.numJoints()), N_(opt.numTimeSteps()), start_(tr.start), goal_(tr.goal)
+    {
+        std::shared_ptr<Policy> ctp;
+        opt.getPolicy(ctp);
+        ok_ = ctp->getControlCosts(R_) && ctp->getParameters(theta_);
+        const int A = N_ + 12;
+        const char* names[3] = {"D0", "D1", "D2"};
+        for (int i = 0; i < 3 && ok_; ++i) {
+            D_[i] = MatrixXd(A, A);
+            ok_ = stomp_engine_get_matrix(opt.engine(), names[i], 0, D_[i].data_.data()) == 0;
+        }
+        w_[0] = q.smoothness_cost_velocity;
+        w_[1] = q.smoothness_cost_acceleration;
+        w_[2] = q.smoothness_cost_jerk;
+    }
+    bool ok() const { return ok_; }
+    bool setNumTimeSteps(const int n) override { return n == N_; }
+    bool getNumTimeSteps(int& n) override { n = N_; return true; }
+    bool getNumDimensions(int& d) override { d = J_; return true; }
+    bool getNumParameters(std::vector<int>& np) override { np.assign(J_, N_); return true; }
+    bool getBasisFunctions(std::vector<MatrixXd>& b) override
+    {
+        MatrixXd I(N_, N_);
+        for (int i = 0; i < N_; ++i) I(i, i) = 1.0;
+        b.assign(J_, I);
+        return true;
+    }
+    bool getControlCosts(std::vector<MatrixXd>& c) override { c = R_; return true; }
+    bool updateParameters(const std::vector<MatrixXd>& u) override
+    {
+        if ((int)u.size() != J_) return false;
+        for (int d = 0; d < J_; ++d)
+            for (int t = 0; t < N_; ++t) theta_[d][t] += u[d](0, t) / 1.0;
+        return true;
+    }
+    bool getParameters(std::vector<VectorXd>& p) override { p = theta_; return true; }
+    bool setParameters(const std::vector<VectorXd>& p) override { theta_ = p; return true; }
+    bool computeControlCosts(const std::vector<MatrixXd>&, const std::vector<std::vector<VectorXd>>&, const double,
+                             std::vector<VectorXd>&) override
+    {
+        return false;   // not used by PolicyImprovement
+    }
+    bool computeControlCosts(const std::vector<MatrixXd>&, const std::vector<VectorXd>& parameters,
+                             const std::vector<VectorXd>& noise, const double weight,
+                             std::vector<VectorXd>& costs) override
+    {
+        const int A = N_ + 12;
+        costs.assign(J_, VectorXd(N_));
+        for (int d = 0; d < J_; ++d) {
+            VectorXd x(A), all(A, 0.0);
+            for (int i = 0; i < A; ++i)
+                x[i] = i < 6 ? start_[d] : (i >= 6 + N_ ? goal_[d] : parameters[d][i - 6] + noise[d][i - 6]);
+            for (int r = 0; r < 3; ++r) {
+                const double w = weight * w_[r];
+                for (int i = 0; i < A; ++i) {
+                    double acc = 0.0;
+                    for (int c = std::max(i - 3, 0); c <= std::min(i + 3, A - 1); ++c) acc += D_[r](i, c) * x[c];
+                    all[i] += w * (acc * acc);
+                }
+            }
+            for (int t = 0; t < N_; ++t) costs[d][t] = all[t + 6];
+            for (int i = 0; i < 6; ++i) {
+                costs[d][0] += all[i];
+                costs[d][N_ - 1] += all[A - (i + 1)];
+            }
+        }
+        return true;
+    }
+
+private:
+    int J_, N_;
+    VectorXd start_, goal_;
+    std::vector<MatrixXd> R_;
+    MatrixXd D_[3];
+    double w_[3];
+    std::vector<VectorXd> theta_;
+    bool ok_ = false;
+};
+
+// A user's Task over that policy: the state costs from the optimizer (stomp_optimizer.cpp:1063-1165)
+class UserTask : public Task {
+public:
+    UserTask(std::shared_ptr<StompOptimizer> o, std::shared_ptr<Policy> p) : o_(std::move(o)), p_(std::move(p)) {}
+    bool initialize(int n) override { return o_->initialize(n); }
+    bool execute(std::vector<VectorXd>& parameters, VectorXd& costs, const int it) override
+    {
+        return o_->execute(parameters, costs, it);
+    }
+    bool executeBatch(std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
+                      const int it) override
+    {
+        return o_->executeBatch(parameters, costs, it);
+    }
+    bool getPolicy(std::shared_ptr<Policy>& policy) override { policy = p_; return true; }
+    bool setPolicy(const std::shared_ptr<Policy> policy) override { p_ = policy; return true; }
+    bool getControlCostWeight(double& w) override { return o_->getControlCostWeight(w); }
+
+private:
+    std::shared_ptr<StompOptimizer> o_;
+    std::shared_ptr<Policy> p_;
+};
+
+// A synthetic policy / task pair with no device: R = tridiagonal (2, -1) + I per dimension,
+// control cost weight * x^2, state cost (x - 1)^2 summed over dimensions
+class ToyPolicy : public Policy {
+public:
+    ToyPolicy(int J, int N) : J_(J), N_(N), theta_(J, VectorXd(N, 0.0)) {}
+    bool setNumTimeSteps(const int n) override { return n == N_; }
+    bool getNumTimeSteps(int& n) override { n = N_; return true; }
+    bool getNumDimensions(int& d) override { d = J_; return true; }
+    bool getNumParameters(std::vector<int>& np) override { np.assign(J_, N_); return true; }
+    bool getBasisFunctions(std::vector<MatrixXd>& b) override { b.assign(J_, MatrixXd(N_, N_)); return true; }
+    bool getControlCosts(std::vector<MatrixXd>& c) override
+    {
+        MatrixXd R(N_, N_);
+        for (int i = 0; i < N_; ++i) {
+            R(i, i) = 3.0;
+            if (i > 0) R(i, i - 1) = -1.0;
+            if (i + 1 < N_) R(i, i + 1) = -1.0;
+        }
+        c.assign(J_, R);
+        return true;
+    }
+    bool updateParameters(const std::vector<MatrixXd>& u) override
+    {
+        for (int d = 0; d < J_; ++d)
+            for (int t = 0; t < N_; ++t) theta_[d][t] += u[d](0, t);
+        return true;
+    }
+    bool getParameters(std::vector<VectorXd>& p) override { p = theta_; return true; }
+    bool setParameters(const std::vector<VectorXd>& p) override { theta_ = p; return true; }
+    bool computeControlCosts(const std::vector<MatrixXd>&, const std::vector<std::vector<VectorXd>>&, const double,
+                             std::vector<VectorXd>&) override
+    {
+        return false;
+    }
+    bool computeControlCosts(const std::vector<MatrixXd>&, const std::vector<VectorXd>& prm,
+                             const std::vector<VectorXd>& nz, const double w, std::vector<VectorXd>& c) override
+    {
+        c.assign(J_, VectorXd(N_));
+        for (int d = 0; d < J_; ++d)
+            for (int t = 0; t < N_; ++t) {
+                const double x = prm[d][t] + nz[d][t];
+                c[d][t] = w * x * x;
+            }
+        return true;
+    }
+
+private:
+    int J_, N_;
+    std::vector<VectorXd> theta_;
+};
+
+class ToyTask : public Task {
+public:
+    explicit ToyTask(std::shared_ptr<Policy> p) : p_(std::move(p)) {}
+    bool initialize(int) override { return true; }
+    bool execute(std::vector<VectorXd>& prm, VectorXd& costs, const int) override
+    {
+        const int N = (int)prm[0].size();
+        costs.assign(N, 0.0);
+        for (const VectorXd& row : prm)
+            for (int t = 0; t < N; ++t) costs[t] += (row[t] - 1.0) * (row[t] - 1.0);
+        return true;
+    }
+    bool getPolicy(std::shared_ptr<Policy>& p) override { p = p_; return true; }
+    bool setPolicy(const std::shared_ptr<Policy> p) override { p_ = p; return true; }
+    bool getControlCostWeight(double& w) override { w = 1e-3; return true; }
+
+private:
+    std::shared_ptr<Policy> p_;
+};
+
 int run_loop(PolicyImprovementLoop& loop, StompOptimizer& opt, std::shared_ptr<Policy> policy, FILE* out)
 {
     for (int it = 1; it <= 10; ++it) {
@@ -149,6 +336,44 @@ int main(int argc, char** argv)
         return 2;
     }
     const std::string mode = argv[3];
+    if (mode == "pi_host_cpu") {
+        // the host PolicyImprovement end to end without a device; the loop must reduce the cost
+        const int J = 3, N = 20;
+        auto policy = std::make_shared<ToyPolicy>(J, N);
+        auto task = std::make_shared<ToyTask>(policy);
+        StompParameters q;
+        q.num_rollouts = 70;   // two 64-rollout summation blocks
+        q.num_reused_rollouts = 7;
+        q.noise_stddev.assign(J, 0.5);
+        q.noise_decay.assign(J, 0.99);
+        PolicyImprovementLoop loop;
+        if (!loop.initialize(task, q)) {
+            std::cerr << loop.lastError() << "\n";
+            return 20;
+        }
+        auto cost = [&]() {
+            std::vector<VectorXd> th;
+            policy->getParameters(th);
+            VectorXd c;
+            task->execute(th, c, 0);
+            double s = 0.0;
+            for (double v : c) s += v;
+            return s;
+        };
+        const double c0 = cost();
+        for (int it = 1; it <= 30; ++it)
+            if (!loop.runSingleIteration(it)) {
+                std::cerr << loop.lastError() << "\n";
+                return 21;
+            }
+        const double c1 = cost();
+        if (!(c1 < 0.5 * c0)) {
+            std::cerr << "host PolicyImprovement did not reduce the cost: " << c0 << " -> " << c1 << "\n";
+            return 22;
+        }
+        std::cout << "pi_host_cpu OK " << c0 << " -> " << c1 << "\n";
+        return 0;
+    }
     if (mode == "validate") {
         // one noise_stddev entry short: the reference would read past the end
         // (policy_improvement_loop.cpp:99-100); the facade refuses
@@ -251,6 +476,68 @@ int main(int argc, char** argv)
             std::vector<std::vector<VectorXd>> extra(1, theta);
             std::vector<VectorXd> extra_cost(1, c);
             if (!pi.addExtraRollouts(extra, extra_cost)) { std::cerr << pi.lastError() << "\n"; return 17; }
+            std::fprintf(out, "%.17g %d %zu\n", opt->lastTrajectoryCost(), opt->lastTrajectoryCollisionFree() ? 1 : 0,
+                         rollouts.size());
+            for (const auto& row : theta) write_vec(out, row);
+            write_vec(out, totals);
+        }
+    } else if (mode == "pi_user") {
+        auto policy = std::make_shared<UserPolicy>(*opt, p.traj, p.params);
+        if (!policy->ok()) return 23;
+        auto task = std::make_shared<UserTask>(opt, policy);
+        PolicyImprovementLoop loop;
+        if (!loop.initialize(task, p.params)) {
+            std::cerr << loop.lastError() << "\n";
+            return 24;
+        }
+        if (int rc = run_loop(loop, *opt, policy, out)) return rc;
+    } else if (mode == "pi_setnum") {
+        if (argc < 6) return 2;
+        int kr = 0;
+        std::ifstream f(argv[5]);
+        f >> kr;
+        if (!f) return 2;
+        std::shared_ptr<Policy> policy;
+        opt->getPolicy(policy);
+        PolicyImprovement pi;
+        const StompParameters& q = p.params;
+        if (!pi.initialize(q.num_rollouts, p.traj.num_points, q.num_reused_rollouts, 1, policy, q.use_cumulative_costs) ||
+            !pi.onEngine()) {
+            std::cerr << pi.lastError() << "\n";
+            return 25;
+        }
+        if (!pi.setNumRollouts(q.num_rollouts, kr, 1) || pi.onEngine()) {
+            std::cerr << "setNumRollouts: " << pi.lastError() << "\n";
+            return 26;
+        }
+        double w = 0.0;
+        opt->getControlCostWeight(w);
+        const int J = p.traj.num_joints, N = p.traj.num_points;
+        for (int it = 1; it <= 10; ++it) {
+            std::vector<double> noise(J);
+            for (int i = 0; i < J; ++i) noise[i] = q.noise_stddev[i] * std::pow(q.noise_decay[i], it - 1);
+            pi.setNoiseIteration(it);
+            std::vector<std::vector<VectorXd>> rollouts;
+            if (!pi.getRollouts(rollouts, noise)) { std::cerr << pi.lastError() << "\n"; return 27; }
+            MatrixXd costs(q.num_rollouts, N);
+            std::vector<VectorXd> c;
+            if (!opt->executeBatch(rollouts, c, it)) return 28;
+            for (size_t r = 0; r < rollouts.size(); ++r)
+                for (int t = 0; t < N; ++t) costs((int)r, t) = c[r][t];
+            std::vector<double> totals;
+            std::vector<MatrixXd> updates;
+            if (!pi.setRolloutCosts(costs, w, totals) || !pi.improvePolicy(updates)) {
+                std::cerr << pi.lastError() << "\n";
+                return 29;
+            }
+            if (!policy->updateParameters(updates)) return 30;
+            std::vector<VectorXd> theta;
+            policy->getParameters(theta);
+            VectorXd cx;
+            if (!opt->execute(theta, cx, it)) return 31;
+            std::vector<std::vector<VectorXd>> extra(1, theta);
+            std::vector<VectorXd> extra_cost(1, cx);
+            if (!pi.addExtraRollouts(extra, extra_cost)) { std::cerr << pi.lastError() << "\n"; return 32; }
             std::fprintf(out, "%.17g %d %zu\n", opt->lastTrajectoryCost(), opt->lastTrajectoryCollisionFree() ? 1 : 0,
                          rollouts.size());
             for (const auto& row : theta) write_vec(out, row);

@@ -49,6 +49,6 @@ def build_driver(directory):
     lib = _build.build_facade()
     exe = os.path.join(directory, "facade_driver")
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"),
-                           os.path.join(ROOT, "tests", "facade_driver.cpp"), "-o", exe, lib,
+                           os.path.join(ROOT, "tests", "facade_driver.cpp"), "-o", exe, lib, _build.LIB,
                            "-Wl,-rpath," + PKG])
     return exe

@@ -161,3 +161,74 @@ def test_facade_compute_control_costs_overloads(tmp_path):
             want[0] += call[i]
             want[N - 1] += call[N + 12 - (i + 1)]
         np.testing.assert_array_equal(vals[1][d], want, err_msg=f"joint {d}")
+
+
+def test_facade_host_policy_improvement_cpu(tmp_path):
+    # PolicyImprovement on the host for a Policy that is not a StompOptimizer's (no device)
+    p = pb.make_problem(grid_n=16, num_rollouts=10, num_reused_rollouts=5)
+    prob, sdf = fu.write_problem(p, str(tmp_path))
+    exe = fu.build_driver(str(tmp_path))
+    r = subprocess.run([exe, prob, sdf, "pi_host_cpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "pi_host_cpu OK" in r.stdout
+
+
+def _theta_cost_rows(toks, J, N, iters, extra=0):
+    pos, rows = 0, []
+    for _ in range(iters):
+        head = toks[pos:pos + 2 + extra]
+        pos += 2 + extra
+        th = np.array([float(x) for x in toks[pos:pos + J * N]]).reshape(J, N)
+        pos += J * N
+        rows.append((float(head[0]), bool(int(head[1])), th, [int(h) for h in head[2:]]))
+    return rows, pos
+
+
+@pytest.mark.gpu
+def test_facade_user_policy_matches_oracle(tmp_path):
+    # a user Policy (theta on the host) and a user Task through PolicyImprovementLoop: the host
+    # PolicyImprovement path, bit for bit the oracle's iterations (reuse included)
+    p = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=4)
+    prob, sdf = fu.write_problem(p, str(tmp_path))
+    exe = fu.build_driver(str(tmp_path))
+    res = str(tmp_path / "out.txt")
+    r = subprocess.run([exe, prob, sdf, "pi_user", res], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    rows, _ = _theta_cost_rows(open(res).read().split(), p.J, p.N, 10)
+    o = po.Oracle(p)
+    for it, (cost, cf, th, _) in enumerate(rows, start=1):
+        oc, ocf = o.iterate(it)
+        assert (cost, cf) == (oc, ocf), it
+        np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it}")
+
+
+@pytest.mark.gpu
+def test_facade_set_num_rollouts_moves_to_host(tmp_path):
+    # setNumRollouts with a K_r the engine was not created with (policy_improvement.cpp:96-147):
+    # the rollout set continues on the host, bit for bit the oracle configured with that K_r
+    p = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=4)
+    prob, sdf = fu.write_problem(p, str(tmp_path))
+    exe = fu.build_driver(str(tmp_path))
+    res, inp = str(tmp_path / "out.txt"), str(tmp_path / "in.txt")
+    with open(inp, "w") as f:
+        f.write("7\n")
+    r = subprocess.run([exe, prob, sdf, "pi_setnum", res, inp], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    toks = open(res).read().split()
+    q = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=7)
+    q.sdf = p.sdf
+    o = po.Oracle(q)
+    K, pos = 12, 0
+    for it in range(1, 11):
+        cost, cf, ngen = float(toks[pos]), bool(int(toks[pos + 1])), int(toks[pos + 2])
+        pos += 3
+        oc, ocf = o.iterate(it)
+        assert (cost, cf) == (oc, ocf), it
+        assert ngen == (K if it == 1 else K - 7)
+        th = np.array([float(x) for x in toks[pos:pos + p.J * p.N]]).reshape(p.J, p.N)
+        pos += p.J * p.N
+        np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it}")
+        totals = np.array([float(x) for x in toks[pos:pos + K]])
+        pos += K
+        st, ct = o.rollouts("state_costs"), o.rollouts("control_costs")
+        np.testing.assert_array_equal(totals, [_getcost(st[k], ct[k]) for k in range(K)])

@@ -74,9 +74,11 @@ def test_facade_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "facade_driver_san")
     subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-Wall", "-fno-omit-frame-pointer",
                            "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                           "-I", os.path.join(ROOT, "include"),
+                           "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "stomp_motion_planner_icra2011_amd", "csrc"),
                            os.path.join(ROOT, "tests", "facade_driver.cpp"),
                            os.path.join(ROOT, "stomp_motion_planner_icra2011_amd", "facade", "stomp_facade.cpp"),
+                           os.path.join(ROOT, "stomp_motion_planner_icra2011_amd", "csrc", "setup.cpp"),
                            "-o", exe, lib, "-Wl,-rpath," + os.path.dirname(lib)])
     p = pb.make_problem(grid_n=16, num_rollouts=10, num_reused_rollouts=5)
     prob, sdf = fu.write_problem(p, str(tmp_path))
@@ -85,4 +87,9 @@ def test_facade_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe, prob, sdf, "validate"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "validate OK" in r.stdout
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
+    # the host PolicyImprovement (any Policy) end to end, no device
+    r = subprocess.run([exe, prob, sdf, "pi_host_cpu"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "pi_host_cpu OK" in r.stdout
     assert "runtime error" not in r.stderr, r.stderr[-4000:]
