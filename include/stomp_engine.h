@@ -280,18 +280,26 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
  *   STOMP_BODY_SPHERE     dims = (radius, -, -)
  *   STOMP_BODY_BOX        dims = (dx, dy, dz)
  *   STOMP_BODY_CYLINDER   dims = (radius, length, -)
- * on the lattice position + g * res around the bounding sphere, kept where the body contains
- * the point (the reference's ray-crossing parity for these convex primitives). */
+ *   STOMP_BODY_MESH       vertices (num_vertices x 3, the body frame, scale applied), dims =
+ *                         (padding, -, -): a robot link's mesh or an environment object of type
+ *                         MESH (:216-223 take it through getVoxelsInBody too), as
+ *                         bodies::ConvexMesh: the convex hull of the vertices
+ * on the lattice position + g * res around the bounding sphere (a mesh's: around its vertices'
+ * bounding-box centre), kept where the body contains the point (the reference's ray-crossing
+ * parity for these convex bodies). */
 #define STOMP_SHAPE_BOX 0
 #define STOMP_SHAPE_CYLINDER 1
 #define STOMP_BODY_SPHERE 2
 #define STOMP_BODY_BOX 3
 #define STOMP_BODY_CYLINDER 4
+#define STOMP_BODY_MESH 5
 typedef struct stomp_shape {
     int32_t type;
     double position[3];
     double orientation[4];      /* quaternion (x, y, z, w), geometry_msgs::Pose order */
     double dims[3];
+    const double* vertices;     /* STOMP_BODY_MESH only (host memory), else NULL */
+    int32_t num_vertices;
 } stomp_shape;
 
 /* The reference's distance-field fill (StompCollisionSpace::setStartState,
@@ -300,8 +308,7 @@ typedef struct stomp_shape {
  * round((p - origin) * (1/res)) when it lies in the grid (PropagationDistanceField::
  * addPointsToField); value = min(d2, cap^2) with cap = ceil(max_expansion/res) (<= 255) and
  * d2 the integer squared cell distance to the nearest marked cell (stomp_grid's
- * representation).  marked (may be NULL): points that landed inside the grid.  Meshes are not
- * supported. */
+ * representation).  marked (may be NULL): points that landed inside the grid. */
 int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* origin, double resolution,
                             double max_expansion, const stomp_shape* shapes, int32_t n_shapes,
                             const double* points, int64_t n_points, uint16_t* out_device, int64_t* marked,

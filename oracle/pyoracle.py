@@ -119,6 +119,8 @@ def lib():
                                            C.POINTER(so_shape), C.c_int, dp, C.c_longlong,
                                            C.POINTER(C.c_ubyte), C.POINTER(C.c_uint16)]
         l.so_sdf_from_occupancy.restype = C.c_int
+        l.so_hull_planes.restype = C.c_int
+        l.so_hull_planes.argtypes = [dp, C.c_int, dp, C.c_int]
         l.so_sdf_from_occupancy.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                             C.POINTER(C.c_ubyte), C.POINTER(C.c_uint16)]
         _lib = l
@@ -127,7 +129,7 @@ def lib():
 
 class so_shape(C.Structure):
     _fields_ = [("type", C.c_int), ("position", C.c_double * 3), ("orientation", C.c_double * 4),
-                ("dims", C.c_double * 3)]
+                ("dims", C.c_double * 3), ("vertices", C.POINTER(C.c_double)), ("num_vertices", C.c_int)]
 
 
 def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
@@ -135,12 +137,18 @@ def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
     marks n^3 uint8, number of points marked)."""
     n = grid.n
     arr = (so_shape * max(len(objects), 1))()
+    keep = []
     for i, o in enumerate(objects):
         arr[i].type = int(o.type)
         arr[i].position[:] = [float(v) for v in o.position]
         arr[i].orientation[:] = [float(v) for v in o.orientation]
         d = list(o.dims) + [0.0] * (3 - len(o.dims))
         arr[i].dims[:] = [float(v) for v in d[:3]]
+        if getattr(o, "vertices", None) is not None:
+            v = np.ascontiguousarray(o.vertices, np.float64).reshape(-1, 3)
+            keep.append(v)
+            arr[i].vertices = _dp(v)
+            arr[i].num_vertices = len(v)
     pts = np.ascontiguousarray(points if points is not None else np.zeros((0, 3)), np.float64).reshape(-1, 3)
     occ = np.zeros((n, n, n), np.uint8)
     field = np.zeros((n, n, n), np.uint16) if with_field else None
@@ -152,6 +160,17 @@ def sdf_build_objects(grid, objects, points=None, with_field: bool = True):
     if marked < 0:
         raise ValueError("so_sdf_build_objects: invalid input")
     return field, occ, int(marked)
+
+
+def hull_planes(vertices) -> np.ndarray:
+    """so_hull_planes: the supporting planes (nx, ny, nz, d) of the vertices' convex hull."""
+    v = np.ascontiguousarray(vertices, np.float64).reshape(-1, 3)
+    cap = 2 * len(v) * len(v) + 8
+    out = np.zeros((cap, 4), np.float64)
+    n = lib().so_hull_planes(_dp(v), len(v), _dp(out), cap)
+    if n < 0:
+        raise ValueError("so_hull_planes: the vertices span no volume")
+    return out[:n].copy()
 
 
 def sdf_from_occupancy(occ: np.ndarray, resolution: float, max_expansion: float) -> np.ndarray:

@@ -18,7 +18,11 @@
  *     counts the crossings of a +z ray (:636-643); for the convex primitives (sphere, box,
  *     cylinder) an odd count is containment, restated here as geometric_shapes'
  *     Body::containsPoint with the pose from btMatrix3x3::setRotation (third party, not
- *     vendored: points exactly on a surface are parity unpinned).
+ *     vendored: points exactly on a surface are parity unpinned).  A mesh (a robot link's, or an
+ *     environment object of type MESH, :216-223, which takes the same getVoxelsInBody path)
+ *     becomes bodies::ConvexMesh: the convex hull of its vertices, whose ray-crossing parity is
+ *     containment in the hull; restated as "inside every supporting plane" (so_hull_planes), the
+ *     lattice centred on the bounding sphere around the vertices' bounding-box centre.
  *  3. distance_field::PropagationDistanceField::addPointsToField (third party): every point
  *     marks the cell round((p - origin) * (1/res)) when all three indices are in [0, n); the
  *     field is the capped exact EDT to the marked cells, stored as min(d2, cap^2) with
@@ -36,7 +40,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { SHAPE_BOX = 0, SHAPE_CYLINDER = 1, BODY_SPHERE = 2, BODY_BOX = 3, BODY_CYLINDER = 4 };
+enum { SHAPE_BOX = 0, SHAPE_CYLINDER = 1, BODY_SPHERE = 2, BODY_BOX = 3, BODY_CYLINDER = 4, BODY_MESH = 5 };
 
 /* KDL Rotation::Quaternion(x, y, z, w) (orocos KDL frames.cpp), row-major */
 static void kdl_rot_quaternion(double x, double y, double z, double w, double* R)
@@ -120,6 +124,77 @@ static double dotcol(const double* v, const double* B, int k)
     return v[0] * B[k] + v[1] * B[3 + k] + v[2] * B[6 + k];
 }
 
+/* supporting planes of the convex hull of V: every vertex triple i < j < k in order spans a
+ * candidate plane n = (vj - vi) x (vk - vi) / |.|, d = -(n . vi); it is kept (flipped so that
+ * the hull lies on the negative side) when no vertex lies more than eps on each side of it,
+ * unless a kept plane already has the same normal (n . n' > 1 - 1e-12) and offset (within eps).
+ * eps = 1e-9 (1 + max |coordinate|).  Deterministic: the engine runs the same loops. */
+int so_hull_planes(const double* V, int nv, double* planes, int max_planes)
+{
+    double ext = 0.0;
+    for (int i = 0; i < 3 * nv; ++i)
+        if (fabs(V[i]) > ext) ext = fabs(V[i]);
+    const double eps = 1e-9 * (1.0 + ext);
+    int np = 0;
+    for (int i = 0; i < nv; ++i)
+        for (int j = i + 1; j < nv; ++j)
+            for (int k = j + 1; k < nv; ++k) {
+                const double* a = V + 3 * i;
+                const double* b = V + 3 * j;
+                const double* c = V + 3 * k;
+                const double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+                const double w[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+                double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+                const double len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+                if (!(len > eps * eps)) continue;   /* (nearly) collinear */
+                n[0] /= len; n[1] /= len; n[2] /= len;
+                double d = -(n[0] * a[0] + n[1] * a[1] + n[2] * a[2]);
+                double smax = -1e300, smin = 1e300;
+                for (int q = 0; q < nv; ++q) {
+                    const double sd = n[0] * V[3 * q] + n[1] * V[3 * q + 1] + n[2] * V[3 * q + 2] + d;
+                    if (sd > smax) smax = sd;
+                    if (sd < smin) smin = sd;
+                }
+                if (smax <= eps) {
+                    /* hull below the plane */
+                } else if (smin >= -eps) {
+                    n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; d = -d;
+                } else {
+                    continue;
+                }
+                int dup = 0;
+                for (int p = 0; p < np && !dup; ++p) {
+                    const double* e = planes + 4 * p;
+                    dup = n[0] * e[0] + n[1] * e[1] + n[2] * e[2] > 1.0 - 1e-12 && fabs(d - e[3]) <= eps;
+                }
+                if (dup) continue;
+                if (np == max_planes) return -1;
+                planes[4 * np] = n[0]; planes[4 * np + 1] = n[1]; planes[4 * np + 2] = n[2]; planes[4 * np + 3] = d;
+                ++np;
+            }
+    return np >= 4 ? np : -1;
+}
+
+/* the mesh body: centre of the vertices' bounding box and the largest distance of a vertex from
+ * it (bodies::ConvexMesh's bounding sphere before the pose; third party, parity unpinned) */
+static void mesh_box_sphere(const double* V, int nv, double* centre, double* radius)
+{
+    double lo[3] = {V[0], V[1], V[2]}, hi[3] = {V[0], V[1], V[2]};
+    for (int q = 1; q < nv; ++q)
+        for (int a = 0; a < 3; ++a) {
+            if (V[3 * q + a] < lo[a]) lo[a] = V[3 * q + a];
+            if (V[3 * q + a] > hi[a]) hi[a] = V[3 * q + a];
+        }
+    for (int a = 0; a < 3; ++a) centre[a] = (lo[a] + hi[a]) / 2.0;
+    double r2 = 0.0;
+    for (int q = 0; q < nv; ++q) {
+        const double dx = V[3 * q] - centre[0], dy = V[3 * q + 1] - centre[1], dz = V[3 * q + 2] - centre[2];
+        const double s = dx * dx + dy * dy + dz * dz;
+        if (s > r2) r2 = s;
+    }
+    *radius = sqrt(r2);
+}
+
 static int body_contains(int type, const double* c, const double* B, const double* d, const double* p)
 {
     const double v[3] = {p[0] - c[0], p[1] - c[1], p[2] - c[2]};
@@ -151,6 +226,51 @@ static double body_bounding_radius(int type, const double* d)
     }
     const double h = d[1] / 2.0;
     return sqrt(d[0] * d[0] + h * h);
+}
+
+/* getVoxelsInBody (:592-650) for a mesh: the lattice around the bounding sphere, a point kept
+ * when, in the body frame (v = w - position, components v . basis column), it lies inside every
+ * hull plane grown by the padding */
+static int mesh_body(marker* mk, const so_shape* s, double res)
+{
+    if (!s->vertices || s->num_vertices < 4) return -1;
+    const int nv = s->num_vertices;
+    const int maxp = 2 * nv * nv + 8;
+    double* planes = (double*)malloc(sizeof(double) * 4 * (size_t)maxp);
+    const int np = so_hull_planes(s->vertices, nv, planes, maxp);
+    if (np < 0) {
+        free(planes);
+        return -1;
+    }
+    double B[9];
+    bt_rot_quaternion(s->orientation[0], s->orientation[1], s->orientation[2], s->orientation[3], B);
+    double bc[3], rb;
+    mesh_box_sphere(s->vertices, nv, bc, &rb);
+    const double pad = s->dims[0];
+    const double* pos = s->position;
+    double c[3];
+    for (int a = 0; a < 3; ++a) c[a] = B[3 * a] * bc[0] + B[3 * a + 1] * bc[1] + B[3 * a + 2] * bc[2] + pos[a];
+    const double r = rb + pad;
+    int lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = (int)(((c[a] - r) - c[a]) * (1.0 / res));
+        hi[a] = (int)(((c[a] + r) - c[a]) * (1.0 / res));
+    }
+    for (int x = lo[0]; x <= hi[0]; ++x)
+        for (int y = lo[1]; y <= hi[1]; ++y)
+            for (int z = lo[2]; z <= hi[2]; ++z) {
+                const double w[3] = {x * res + c[0], y * res + c[1], z * res + c[2]};   /* gridToWorld */
+                const double v[3] = {w[0] - pos[0], w[1] - pos[1], w[2] - pos[2]};
+                const double pb[3] = {dotcol(v, B, 0), dotcol(v, B, 1), dotcol(v, B, 2)};
+                int in = 1;
+                for (int p = 0; p < np && in; ++p) {
+                    const double* e = planes + 4 * p;
+                    in = !(e[0] * pb[0] + e[1] * pb[1] + e[2] * pb[2] + e[3] > pad);
+                }
+                if (in) mark(mk, w[0], w[1], w[2]);
+            }
+    free(planes);
+    return 0;
 }
 
 /* getVoxelsInBody (:592-650) */
@@ -244,7 +364,12 @@ long long so_sdf_build_objects(int nx, int ny, int nz, const double* origin, dou
     for (int s = 0; s < n_shapes; ++s) {
         if (shapes[s].type == SHAPE_BOX || shapes[s].type == SHAPE_CYLINDER) env_shape(&mk, &shapes[s], res);
         else if (shapes[s].type >= BODY_SPHERE && shapes[s].type <= BODY_CYLINDER) robot_body(&mk, &shapes[s], res);
-        else {
+        else if (shapes[s].type == BODY_MESH) {
+            if (mesh_body(&mk, &shapes[s], res) != 0) {
+                free(own);
+                return -1;
+            }
+        } else {
             free(own);
             return -1;
         }

@@ -207,6 +207,8 @@ typedef struct {
     double position[3];
     double orientation[4];   /* quaternion x, y, z, w */
     double dims[3];
+    const double* vertices;  /* BODY_MESH: num_vertices x 3 in the body frame (scale applied); dims[0] = padding */
+    int num_vertices;
 } so_shape;
 /* occ (nx*ny*nz bytes, may be NULL) receives the marked cells; sdf (uint16, may be NULL) the
  * field min(d2, cap^2), cap = ceil(max_expansion / res) <= 255.  Returns the number of points
@@ -214,6 +216,10 @@ typedef struct {
 long long so_sdf_build_objects(int nx, int ny, int nz, const double* origin, double res, double max_expansion,
                                const so_shape* shapes, int n_shapes, const double* points, long long n_points,
                                unsigned char* occ, unsigned short* sdf);
+/* bodies::ConvexMesh's hull as planes: the supporting planes (unit outward normal n, offset d:
+ * n.x + d = 0 on the face) of the convex hull of V (nv x 3); planes: room for max_planes x 4.
+ * Returns the number of planes, -1 if the vertices span no volume or max_planes is too small. */
+int so_hull_planes(const double* V, int nv, double* planes, int max_planes);
 /* capped EDT of an occupancy grid alone (the second half of so_sdf_build_objects); -1 when the
  * cap exceeds 255 cells (d2 would not fit 16 bits) */
 int so_sdf_from_occupancy(int nx, int ny, int nz, double res, double max_expansion, const unsigned char* occ,

@@ -1911,6 +1911,86 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
     return 0;
 }
 
+// bodies::ConvexMesh's convex hull (third party: qhull in geometric_shapes) as its supporting
+// planes, appended to `planes` as (n, d) with unit outward n and n.x + d = 0 on the face: every
+// vertex triple i < j < k in order spans a candidate plane, kept (flipped so the hull lies on the
+// negative side) when no vertex lies more than eps on each side of it, unless a kept plane has
+// the same normal and offset.  eps = 1e-9 (1 + max |coordinate|).  Returns the number of planes
+// (-1: no volume).  oracle/sdf_oracle.c so_hull_planes runs the same loops.
+static int hull_planes(const double* V, int nv, std::vector<double>& planes)
+{
+    double ext = 0.0;
+    for (int i = 0; i < 3 * nv; ++i)
+        if (std::fabs(V[i]) > ext) ext = std::fabs(V[i]);
+    const double eps = 1e-9 * (1.0 + ext);
+    const size_t first = planes.size();
+    int np = 0;
+    for (int i = 0; i < nv; ++i)
+        for (int j = i + 1; j < nv; ++j)
+            for (int k = j + 1; k < nv; ++k) {
+                const double* a = V + 3 * i;
+                const double* b = V + 3 * j;
+                const double* c = V + 3 * k;
+                const double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+                const double w[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+                double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+                const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+                if (!(len > eps * eps)) continue;
+                n[0] /= len;
+                n[1] /= len;
+                n[2] /= len;
+                double d = -(n[0] * a[0] + n[1] * a[1] + n[2] * a[2]);
+                double smax = -1e300, smin = 1e300;
+                for (int q = 0; q < nv; ++q) {
+                    const double sd = n[0] * V[3 * q] + n[1] * V[3 * q + 1] + n[2] * V[3 * q + 2] + d;
+                    if (sd > smax) smax = sd;
+                    if (sd < smin) smin = sd;
+                }
+                if (smax <= eps) {
+                } else if (smin >= -eps) {
+                    n[0] = -n[0];
+                    n[1] = -n[1];
+                    n[2] = -n[2];
+                    d = -d;
+                } else {
+                    continue;
+                }
+                bool dup = false;
+                for (int p = 0; p < np && !dup; ++p) {
+                    const double* e = planes.data() + first + 4 * p;
+                    dup = n[0] * e[0] + n[1] * e[1] + n[2] * e[2] > 1.0 - 1e-12 && std::fabs(d - e[3]) <= eps;
+                }
+                if (dup) continue;
+                planes.insert(planes.end(), {n[0], n[1], n[2], d});
+                ++np;
+            }
+    if (np < 4) {
+        planes.resize(first);
+        return -1;
+    }
+    return np;
+}
+
+// the vertices' bounding-box centre and the largest distance of a vertex from it (bodies::
+// ConvexMesh's bounding sphere before the pose; third party, parity unpinned)
+static void mesh_box_sphere(const double* V, int nv, double* centre, double* radius)
+{
+    double lo[3] = {V[0], V[1], V[2]}, hi[3] = {V[0], V[1], V[2]};
+    for (int q = 1; q < nv; ++q)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], V[3 * q + a]);
+            hi[a] = std::max(hi[a], V[3 * q + a]);
+        }
+    for (int a = 0; a < 3; ++a) centre[a] = (lo[a] + hi[a]) / 2.0;
+    double r2 = 0.0;
+    for (int q = 0; q < nv; ++q) {
+        const double dx = V[3 * q] - centre[0], dy = V[3 * q + 1] - centre[1], dz = V[3 * q + 2] - centre[2];
+        const double s = dx * dx + dy * dy + dz * dz;
+        if (s > r2) r2 = s;
+    }
+    *radius = std::sqrt(r2);
+}
+
 // StompCollisionSpace::setStartState's fill (stomp_collision_space.cpp:154-297, 564-650): the
 // per-object lattice is set up here (the environment objects' coordinate lists by the reference's
 // own running-sum loops), the marking and the EDT run on the device (k_sdf.hip)
@@ -1925,6 +2005,7 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
     if (!(capd >= 0) || capd > 255) return fail(nullptr, STOMP_E_UNSUPPORTED, "max_expansion / resolution above 255 cells");
     const int cap = (int)capd;
     std::vector<double> axes;
+    std::vector<double> mesh_planes;   // every mesh's hull planes, 4 doubles each
     std::vector<SdfLatticeJob> jobs;
     const long long kMaxLattice = 1LL << 31;
     for (int s = 0; s < n_shapes; ++s) {
@@ -1963,7 +2044,7 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
                 npts *= j.n[a];
             }
             if (npts > kMaxLattice) return fail(nullptr, STOMP_E_INVALID, "object %d: lattice too large", s);
-        } else if (sh.type >= STOMP_BODY_SPHERE && sh.type <= STOMP_BODY_CYLINDER) {
+        } else if (sh.type >= STOMP_BODY_SPHERE && sh.type <= STOMP_BODY_MESH) {
             // btMatrix3x3::setRotation (bodies::Body::setPose)
             const double dq = qx * qx + qy * qy + qz * qz + qw * qw;
             const double sc = 2.0 / dq;
@@ -1976,18 +2057,37 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
             std::memcpy(j.R, B, sizeof B);
             const double* d = sh.dims;
             double r;   // bodies::*::computeBoundingSphere
+            double centre[3] = {sh.position[0], sh.position[1], sh.position[2]};
             if (sh.type == STOMP_BODY_SPHERE) {
                 r = d[0];
             } else if (sh.type == STOMP_BODY_BOX) {
                 const double a = d[0] / 2.0, b = d[1] / 2.0, c = d[2] / 2.0;
                 r = std::sqrt(a * a + b * b + c * c);
-            } else {
+            } else if (sh.type == STOMP_BODY_CYLINDER) {
                 const double h = d[1] / 2.0;
                 r = std::sqrt(d[0] * d[0] + h * h);
+            } else {
+                // bodies::ConvexMesh: the convex hull of the vertices as planes, the lattice around
+                // the bounding sphere of the vertices' bounding-box centre
+                if (!sh.vertices || sh.num_vertices < 4)
+                    return fail(nullptr, STOMP_E_INVALID, "mesh %d: needs at least 4 vertices", s);
+                const int first = (int)mesh_planes.size() / 4;
+                const int np = hull_planes(sh.vertices, sh.num_vertices, mesh_planes);
+                if (np < 0) return fail(nullptr, STOMP_E_INVALID, "mesh %d: the vertices span no volume", s);
+                j.nplanes = np;
+                j.off[0] = first;   // plane offset, resolved to a device pointer below
+                double bc[3], rb;
+                mesh_box_sphere(sh.vertices, sh.num_vertices, bc, &rb);
+                for (int a = 0; a < 3; ++a) {
+                    j.org[a] = sh.position[a];
+                    centre[a] = B[3 * a] * bc[0] + B[3 * a + 1] * bc[1] + B[3 * a + 2] * bc[2] + sh.position[a];
+                    j.pos[a] = centre[a];
+                }
+                r = rb + d[0];
             }
             long long npts = 1;
             for (int a = 0; a < 3; ++a) {
-                const double c = sh.position[a];
+                const double c = centre[a];
                 const double lo = ((c - r) - c) * (1.0 / res), hi = ((c + r) - c) * (1.0 / res);
                 if (!(std::fabs(lo) < 1e9 && std::fabs(hi) < 1e9))
                     return fail(nullptr, STOMP_E_INVALID, "body %d: lattice too large", s);
@@ -2006,7 +2106,7 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
     const size_t cells = (size_t)nx * ny * nz;
     unsigned char* occ = nullptr;
     unsigned short *a = nullptr, *b = nullptr;
-    double *d_axes = nullptr, *d_pts = nullptr;
+    double *d_axes = nullptr, *d_pts = nullptr, *d_planes = nullptr;
     unsigned long long* d_marked = nullptr;
     auto cleanup = [&]() {
         if (occ) hipFree(occ);
@@ -2014,19 +2114,29 @@ int stomp_sdf_build_objects(int32_t nx, int32_t ny, int32_t nz, const double* or
         if (b) hipFree(b);
         if (d_axes) hipFree(d_axes);
         if (d_pts) hipFree(d_pts);
+        if (d_planes) hipFree(d_planes);
         if (d_marked) hipFree(d_marked);
     };
     if (hipMalloc(&occ, cells) != hipSuccess || hipMalloc(&a, cells * 2) != hipSuccess ||
         hipMalloc(&b, cells * 2) != hipSuccess || hipMalloc(&d_marked, sizeof(unsigned long long)) != hipSuccess ||
         (!axes.empty() && hipMalloc(&d_axes, axes.size() * sizeof(double)) != hipSuccess) ||
+        (!mesh_planes.empty() && hipMalloc(&d_planes, mesh_planes.size() * sizeof(double)) != hipSuccess) ||
         (n_points > 0 && hipMalloc(&d_pts, (size_t)n_points * 3 * sizeof(double)) != hipSuccess)) {
         cleanup();
         return fail(nullptr, STOMP_E_DEVICE, "sdf build: hipMalloc");
     }
+    for (SdfLatticeJob& j : jobs)
+        if (j.type == kBodyMesh) {
+            j.planes = d_planes + 4 * (size_t)j.off[0];
+            j.off[0] = 0;
+        }
     hipError_t err = hipMemsetAsync(occ, 0, cells, st);
     if (err == hipSuccess) err = hipMemsetAsync(d_marked, 0, sizeof(unsigned long long), st);
     if (err == hipSuccess && d_axes)
         err = hipMemcpyAsync(d_axes, axes.data(), axes.size() * sizeof(double), hipMemcpyHostToDevice, st);
+    if (err == hipSuccess && d_planes)
+        err = hipMemcpyAsync(d_planes, mesh_planes.data(), mesh_planes.size() * sizeof(double), hipMemcpyHostToDevice,
+                             st);
     if (err == hipSuccess && d_pts)
         err = hipMemcpyAsync(d_pts, points, (size_t)n_points * 3 * sizeof(double), hipMemcpyHostToDevice, st);
     if (err != hipSuccess) {

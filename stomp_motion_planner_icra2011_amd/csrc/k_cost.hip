@@ -243,53 +243,86 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         else if (v < jmin) absamt = fabs(jmin - v);
         any |= absamt > 1e-6;
     }
-    // Joints are independent, so each wave owns joints wv, wv + NW, ...: the argmax is a
-    // wave butterfly (every lane ends with the same (max, first index)) and a pass needs
-    // no block barrier.  LDS accesses of one wave execute in program order.
+    // Joints are independent: the limited joints are dealt round-robin over the waves and a wave
+    // runs the passes of two of its joints in lockstep (pass p of one beside pass p of the other,
+    // each joint still stopping on its own), so the two Q^-1 column loads of a step are in flight
+    // together.  The argmax is a wave butterfly (every lane ends with the same (max, first
+    // index)) and a pass needs no block barrier: LDS accesses of one wave execute in program order.
     if (__syncthreads_or(any)) {
-        __builtin_amdgcn_s_setprio(3);   // one wave per limited joint: a dependent chain (critical path)
-        for (int j = wv; j < J; j += NW) {
-            if (!hl_s[j]) continue;
+        __builtin_amdgcn_s_setprio(3);   // a dependent chain per joint (critical path)
+        // the violated waypoint a pass of joint j corrects (wave-uniform), -1 when none is left
+        auto jl_argmax = [&](int j) -> int {
             const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
-            const double* Q = m.QT + (size_t)j * N * N;
+            const double* tj = traj + j * N;
+            double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
+            int ci = 0;
+            for (int t = lane; t < N; t += 64) {
+                const double v = tj[t];
+                double absamt = 0.0;
+                if (v > jmax) absamt = fabs(jmax - v);
+                else if (v < jmin) absamt = fabs(jmin - v);
+                if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
+            }
+            // wave argmax, first index on ties: the bits of a non-negative double order like
+            // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
+            const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
+            const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
+            const unsigned mh = wave_max_u32(hi);
+            const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
+            if ((mh | ml) == 0u) return -1;   // no violation left (wave-uniform)
+            const bool match = hi == mh && lo == ml;
+            int cm = 0;
+            for (int blk = 0; blk * 64 < N; ++blk) {
+                const unsigned long long b = __ballot(match && (ci >> 6) == blk);
+                if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
+            }
+            return cm;
+        };
+        // traj_j += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
+        auto jl_apply = [&](int j, int cm, const double* qv, double qd) {
+            const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
             double* tj = traj + j * N;
-            for (int pass = 0; pass < 11; ++pass) {
-                double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
-                int ci = 0;
-                for (int t = lane; t < N; t += 64) {
-                    const double v = tj[t];
-                    double absamt = 0.0;
-                    if (v > jmax) absamt = fabs(jmax - v);
-                    else if (v < jmin) absamt = fabs(jmin - v);
-                    if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
-                }
-                // wave argmax, first index on ties: the bits of a non-negative double order like
-                // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
-                const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
-                const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
-                const unsigned mh = wave_max_u32(hi);
-                const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
-                if ((mh | ml) == 0u) break;   // no violation left (wave-uniform)
-                const bool match = hi == mh && lo == ml;
-                int cm = 0;
-                for (int blk = 0; blk * 64 < N; ++blk) {
-                    const unsigned long long b = __ballot(match && (ci >> 6) == blk);
-                    if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
-                }
-                const double* Qc = Q + (size_t)cm * N;
-                double qv[4];   // the column's loads go out with the diagonal's (N <= 256)
+            const double v = tj[cm];
+            const double amount = v > jmax ? jmax - v : jmin - v;
+            const double mult = amount / qd;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) qv[u] = Qc[min(lane + 64 * u, N - 1)];
-                const double qd = Qc[cm];
-                const double v = tj[cm];
-                const double amount = v > jmax ? jmax - v : jmin - v;
-                const double mult = amount / qd;
+            for (int u = 0; u < 4; ++u)
+                if (lane + 64 * u < N) tj[lane + 64 * u] += mult * qv[u];
+        };
+        auto jl_pair = [&](int ja, int jb) {
+            bool la = true, lb = jb >= 0;
+            for (int pass = 0; pass < 11 && (la || lb); ++pass) {
+                int ca = -1, cb = -1;
+                if (la) { ca = jl_argmax(ja); la = ca >= 0; }
+                if (lb) { cb = jl_argmax(jb); lb = cb >= 0; }
+                if (!la && !lb) break;
+                // both columns and diagonals in flight (unconditional loads, clamped; N <= 256)
+                const double* Qa = m.QT + ((size_t)ja * N + (size_t)max(ca, 0)) * N;
+                const double* Qb = m.QT + ((size_t)max(jb, 0) * N + (size_t)max(cb, 0)) * N;
+                double qa[4], qb[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (lane + 64 * u < N) tj[lane + 64 * u] += mult * qv[u];
+                for (int u = 0; u < 4; ++u) {
+                    qa[u] = Qa[min(lane + 64 * u, N - 1)];
+                    qb[u] = Qb[min(lane + 64 * u, N - 1)];
+                }
+                const double qda = Qa[max(ca, 0)], qdb = Qb[max(cb, 0)];
+                if (la) jl_apply(ja, ca, qa, qda);
+                if (lb) jl_apply(jb, cb, qb, qdb);
                 __builtin_amdgcn_wave_barrier();
             }
+        };
+        int mine = -1, k = 0;
+        for (int j = 0; j < J; ++j) {
+            if (!hl_s[j]) continue;
+            if (k++ % NW != wv) continue;
+            if (mine < 0) {
+                mine = j;
+            } else {
+                jl_pair(mine, j);
+                mine = -1;
+            }
         }
+        if (mine >= 0) jl_pair(mine, -1);
         __builtin_amdgcn_s_setprio(2);
         __syncthreads();
     }

@@ -3,8 +3,9 @@
 //   k_mark_lattice  one lane per lattice point of one object: environment boxes / cylinders
 //                   sampled on the reference's running-sum lattice (addCollisionObjectsToPoints,
 //                   :199-297; the per-axis coordinate lists are made on the host by the same loop),
-//                   robot bodies on the bounding-sphere lattice with a containment test
-//                   (getVoxelsInBody, :592-650); the point goes through the object's frame and
+//                   robot bodies (and meshes: their convex hull's planes) on the bounding-sphere
+//                   lattice with a containment test (getVoxelsInBody, :592-650); the point goes
+//                   through the object's frame and
 //                   marks its cell (PropagationDistanceField::addPointsToField: round((p - o) / res)
 //                   per axis, dropped unless inside the grid)
 //   k_mark_points   the collision-map points (:205-211), marked the same way
@@ -75,7 +76,16 @@ __global__ __launch_bounds__(256) void k_mark_lattice(SdfLatticeJob j, const dou
             const double v[3] = {w[0] - pos[0], w[1] - pos[1], w[2] - pos[2]};
             const double* d = j.dims;
             bool in;
-            if (j.type == kBodySphere) {
+            if (j.type == kBodyMesh) {
+                // bodies::ConvexMesh: inside every hull plane grown by the padding, in the body frame
+                const double u[3] = {w[0] - j.org[0], w[1] - j.org[1], w[2] - j.org[2]};
+                const double pb[3] = {dotcol(u, j.R, 0), dotcol(u, j.R, 1), dotcol(u, j.R, 2)};
+                in = true;
+                for (int q = 0; q < j.nplanes && in; ++q) {
+                    const double* e = j.planes + 4 * q;
+                    in = !(e[0] * pb[0] + e[1] * pb[1] + e[2] * pb[2] + e[3] > d[0]);
+                }
+            } else if (j.type == kBodySphere) {
                 in = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] < d[0] * d[0];
             } else if (j.type == kBodyBox) {
                 in = !(fabs(dotcol(v, j.R, 0)) > d[0] / 2.0) && !(fabs(dotcol(v, j.R, 1)) > d[1] / 2.0) &&

@@ -362,7 +362,7 @@ void launch_sdf_build(int nx, int ny, int nz, int cap2, const int* boxes /*n x 6
                       unsigned short* out, hipStream_t s);
 
 // the reference's object voxeliser (k_sdf.hip); shape types as STOMP_SHAPE_* / STOMP_BODY_*
-constexpr int kShapeBox = 0, kShapeCylinder = 1, kBodySphere = 2, kBodyBox = 3, kBodyCylinder = 4;
+constexpr int kShapeBox = 0, kShapeCylinder = 1, kBodySphere = 2, kBodyBox = 3, kBodyCylinder = 4, kBodyMesh = 5;
 struct SdfMarkArgs {
     int n[3];
     double o[3];
@@ -375,10 +375,13 @@ struct SdfLatticeJob {
     int n[3];                    // lattice points per axis
     int off[3];                  // environment objects: offsets of the axis coordinate lists
     int lo[3];                   // robot bodies: first lattice index per axis
-    double pos[3];
+    double pos[3];               // lattice centre (the bounding sphere's for bodies)
     double R[9];                 // KDL Rotation::Quaternion (objects) / btMatrix3x3 basis (bodies)
     double dims[3];
     double res;
+    double org[3];               // meshes: the body's position (pos is its bounding-sphere centre)
+    const double* planes;        // meshes: nplanes x (n, d) of the convex hull, device memory
+    int nplanes;
 };
 void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMarkArgs& g, hipStream_t s);
 void launch_mark_points(const double* pts, long long np, const SdfMarkArgs& g, hipStream_t s);

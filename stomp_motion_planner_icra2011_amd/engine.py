@@ -28,7 +28,7 @@ class stomp_sphere(C.Structure):
 
 class stomp_shape(C.Structure):
     _fields_ = [("type", C.c_int32), ("position", C.c_double * 3), ("orientation", C.c_double * 4),
-                ("dims", C.c_double * 3)]
+                ("dims", C.c_double * 3), ("vertices", C.POINTER(C.c_double)), ("num_vertices", C.c_int32)]
 
 
 class stomp_joint(C.Structure):
@@ -188,14 +188,21 @@ def sdf_build_device(problem, device_tensor_ptr: int, stream: int = 0):
 
 
 def shape_array(objects):
-    """problem.SceneObject list -> stomp_shape[] (ctypes array; length >= 1)."""
+    """problem.SceneObject list -> stomp_shape[] (ctypes array; length >= 1; it keeps the mesh
+    vertex arrays alive as ._keep)."""
     arr = (stomp_shape * max(len(objects), 1))()
+    arr._keep = []
     for i, o in enumerate(objects):
         arr[i].type = int(o.type)
         arr[i].position[:] = [float(v) for v in o.position]
         arr[i].orientation[:] = [float(v) for v in o.orientation]
         d = list(o.dims) + [0.0] * (3 - len(o.dims))
         arr[i].dims[:] = [float(v) for v in d[:3]]
+        if getattr(o, "vertices", None) is not None:
+            v = np.ascontiguousarray(o.vertices, np.float64).reshape(-1, 3)
+            arr._keep.append(v)
+            arr[i].vertices = _dp(v)
+            arr[i].num_vertices = len(v)
     return arr
 
 

@@ -245,7 +245,7 @@ def shelf_scene(with_pole: bool = True):
 
 # collision-space objects as the reference's voxeliser takes them (stomp_engine.h STOMP_SHAPE_* /
 # STOMP_BODY_*; stomp_collision_space.cpp:199-297, 592-650)
-SHAPE_BOX, SHAPE_CYLINDER, BODY_SPHERE, BODY_BOX, BODY_CYLINDER = 0, 1, 2, 3, 4
+SHAPE_BOX, SHAPE_CYLINDER, BODY_SPHERE, BODY_BOX, BODY_CYLINDER, BODY_MESH = 0, 1, 2, 3, 4, 5
 
 
 @dataclasses.dataclass
@@ -254,6 +254,7 @@ class SceneObject:
     position: Sequence[float]
     orientation: Sequence[float] = (0.0, 0.0, 0.0, 1.0)   # quaternion x, y, z, w
     dims: Sequence[float] = (0.0, 0.0, 0.0)
+    vertices: Optional[np.ndarray] = None   # BODY_MESH: V x 3 in the body frame, scaled; dims[0] = padding
 
 
 def quaternion_from_rpy(roll: float, pitch: float, yaw: float):
@@ -273,6 +274,16 @@ def shelf_objects(with_pole: bool = True) -> List[SceneObject]:
     out = [SceneObject(SHAPE_BOX, tuple(b.center), q, tuple(b.dims)) for b in boxes]
     out += [SceneObject(SHAPE_CYLINDER, tuple(c.center), q, (c.radius, c.length, 0.0)) for c in cyls]
     return out
+
+
+def mesh_object(vertices, triangles=None, position=(0.0, 0.0, 0.0), rpy=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0),
+                padding: float = 0.0) -> SceneObject:
+    """A MESH collision object as the reference's scene files give one (environment_mesh.yaml:
+    position, orientation [roll, pitch, yaw], scale): bodies::ConvexMesh of the scaled vertices
+    (the triangles do not enter the convex hull)."""
+    v = np.asarray(vertices, np.float64).reshape(-1, 3) * np.asarray(scale, np.float64)[None, :]
+    return SceneObject(BODY_MESH, tuple(float(x) for x in position), quaternion_from_rpy(*rpy), (padding, 0.0, 0.0),
+                       np.ascontiguousarray(v))
 
 
 @dataclasses.dataclass

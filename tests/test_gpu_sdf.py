@@ -9,7 +9,7 @@ from stomp_motion_planner_icra2011_amd import problem as pb
 from stomp_motion_planner_icra2011_amd import engine as eng
 from oracle import pyoracle as po
 
-from tests.test_sdf_objects import mixed_scene, small_grid
+from tests.test_sdf_objects import bookshelves_object, mesh_grid, mixed_scene, small_grid
 
 pytestmark = pytest.mark.gpu
 
@@ -88,3 +88,24 @@ def test_invalid_inputs_refused():
     big = pb.Grid(16, grid.origin, 0.001, 1.0)   # cap = 1000 cells > 255
     with pytest.raises(RuntimeError):
         eng.sdf_build_objects_device(big, [], buf.ptr)
+
+
+@pytest.mark.parametrize("n,padding", [(64, 0.0), (128, 0.02)])
+def test_mesh_scene_bitwise(n, padding):
+    # environment_mesh.yaml: the bookshelves mesh (bodies::ConvexMesh) and the box beside it, plus
+    # the mixed primitives, against the oracle
+    grid = mesh_grid(n)
+    objs = [bookshelves_object(padding),
+            pb.SceneObject(pb.SHAPE_BOX, (1.05, 0.7, 0.0), pb.quaternion_from_rpy(0.0, 0.0, -1.57), (1.0, 1.0, 1.0))]
+    want, _, count = po.sdf_build_objects(grid, objs)
+    got, marked = device_field(grid, objs)
+    assert marked == count and count > 1000
+    np.testing.assert_array_equal(got, want)
+
+
+def test_mesh_rejected_on_device():
+    grid = mesh_grid(16)
+    flat = pb.SceneObject(pb.BODY_MESH, (1.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), (0.0, 0.0, 0.0),
+                          np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0]], np.float64))
+    with pytest.raises(RuntimeError):
+        device_field(grid, [flat])

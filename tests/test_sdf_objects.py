@@ -210,3 +210,102 @@ def test_rpy_quaternion_identity_and_unit():
     assert pb.quaternion_from_rpy(0.0, 0.0, 0.0) == (0.0, 0.0, 0.0, 1.0)
     q = pb.quaternion_from_rpy(0.3, -1.2, 2.0)
     assert abs(sum(v * v for v in q) - 1.0) < 1e-15
+
+
+# ---------------------------------------------------------------- meshes (bodies::ConvexMesh)
+
+def _meshes():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "meshes.npz"))
+
+
+def bookshelves_object(padding=0.0):
+    """environment_mesh.yaml's bookshelves: position, RPY orientation and scale of the scene file
+    (the mesh data: tests/golden/meshes.npz, made by tools/extract_mesh.py)."""
+    m = _meshes()
+    return pb.mesh_object(m["bookshelves_vertices"], m["bookshelves_triangles"], tuple(m["bookshelves_position"]),
+                          tuple(m["bookshelves_rpy"]), tuple(m["bookshelves_scale"]), padding)
+
+
+@pytest.mark.parametrize("name,scale", [("bookshelves", 0.031), ("cabnite", 0.001)])
+def test_hull_planes_match_qhull(name, scale):
+    # the reference's ConvexMesh is qhull's hull of the vertices; scipy's ConvexHull is qhull
+    from scipy.spatial import ConvexHull
+    v = _meshes()[name + "_vertices"] * scale
+    ours = po.hull_planes(v)
+    h = ConvexHull(v)
+    uniq = []
+    for e in h.equations:
+        if not any(abs(float(np.dot(e[:3], u[:3])) - 1.0) < 1e-9 and abs(e[3] - u[3]) < 1e-9 for u in uniq):
+            uniq.append(e)
+    assert len(ours) == len(uniq)
+    for e in uniq:
+        assert any(abs(float(np.dot(e[:3], u[:3])) - 1.0) < 1e-9 and abs(e[3] - u[3]) < 1e-9 for u in ours)
+    rng = np.random.default_rng(3)
+    P = rng.uniform(v.min(0) - 0.05, v.max(0) + 0.05, (50000, 3))
+    a = np.all(P @ ours[:, :3].T + ours[:, 3] <= 0, axis=1)
+    b = np.all(P @ h.equations[:, :3].T + h.equations[:, 3] <= 0, axis=1)
+    assert np.array_equal(a, b) and a.sum() > 1000
+
+
+def mesh_reference_marks(grid, o):
+    """getVoxelsInBody (:592-650) for a mesh body, transcribed: the bounding-sphere lattice around
+    the vertices' bounding-box centre (through the pose), a point kept inside every hull plane
+    grown by the padding (ray-crossing parity of a convex body), marked as addPointsToField does"""
+    v = np.asarray(o.vertices, np.float64)
+    planes = po.hull_planes(v)
+    B = bt_quaternion(*o.orientation)
+    lo_b, hi_b = v.min(0), v.max(0)
+    bc = [(lo_b[a] + hi_b[a]) / 2.0 for a in range(3)]
+    rb = math.sqrt(max(sum((float(x[a]) - bc[a]) ** 2 for a in range(3)) for x in v))
+    pad, pos, res = o.dims[0], o.position, grid.resolution
+    c = [B[3 * a] * bc[0] + B[3 * a + 1] * bc[1] + B[3 * a + 2] * bc[2] + pos[a] for a in range(3)]
+    r = rb + pad
+    lo = [int(((ca - r) - ca) * (1.0 / res)) for ca in c]
+    hi = [int(((ca + r) - ca) * (1.0 / res)) for ca in c]
+    g = np.stack(np.meshgrid(*[np.arange(lo[a], hi[a] + 1) for a in range(3)], indexing="ij"), -1).reshape(-1, 3)
+    w = g * res + np.array(c)
+    u = w - np.array(pos)
+    Bm = np.array(B).reshape(3, 3)
+    pbody = u @ Bm   # components u . basis column k
+    inside = np.all(pbody @ planes[:, :3].T + planes[:, 3] <= pad, axis=1)
+    n, o_, inv = grid.n, grid.origin, 1.0 / grid.resolution
+    occ = np.zeros((n, n, n), np.uint8)
+    cnt = 0
+    for p in w[inside]:
+        cc = [c_round((p[a] - o_[a]) * inv) for a in range(3)]
+        if all(0.0 <= cc[a] < n for a in range(3)):
+            occ[int(cc[0]), int(cc[1]), int(cc[2])] = 1
+            cnt += 1
+    return occ, cnt
+
+
+def mesh_grid(n=48):
+    # a cube around the bookshelves of environment_mesh.yaml (base_footprint frame)
+    return pb.Grid(n, (0.3, -0.4, -0.3), 2.0 / n, 0.17)
+
+
+@pytest.mark.parametrize("padding", [0.0, 0.03])
+def test_mesh_body_marks_follow_the_reference_loop(padding):
+    grid = mesh_grid()
+    o = bookshelves_object(padding)
+    want, count = mesh_reference_marks(grid, o)
+    _, occ, marked = po.sdf_build_objects(grid, [o], with_field=False)
+    assert marked == count and count > 500
+    np.testing.assert_array_equal(occ, want)
+
+
+def test_mesh_scene_field_is_edt_of_marks():
+    grid = mesh_grid(32)
+    objs = [bookshelves_object(), pb.SceneObject(pb.SHAPE_BOX, (1.05, 0.7, 0.0), pb.quaternion_from_rpy(0.0, 0.0, -1.57),
+                                                 (1.0, 1.0, 1.0))]
+    field, occ, _ = po.sdf_build_objects(grid, objs)
+    np.testing.assert_array_equal(field, brute_force_edt(occ, grid.resolution, grid.max_expansion))
+
+
+def test_mesh_rejects_flat_vertices():
+    grid = mesh_grid(16)
+    flat = pb.SceneObject(pb.BODY_MESH, (1.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), (0.0, 0.0, 0.0),
+                          np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0]], np.float64))
+    with pytest.raises(ValueError):
+        po.sdf_build_objects(grid, [flat])
