@@ -126,15 +126,19 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // one value where floor(u + 0.5) != round(u) for u >= 0, u = 0.5 - 2^-54, is below 0.5 and
 // rejected by the range test).  So the range test moves onto u and each axis costs sub, mul,
 // two compares, add and floor.
-// The voxel index of p (cell 0 when p reads distance 0: ok = false).
+// The voxel index of p (cell 0 when p reads distance 0: ok = false).  After u = (p - o) * (1/res)
+// in double, the rest is integer work: for u >= 0.5, trunc(u + 0.5) = floor(u + 0.5) = round(u)
+// (see above), and the range test moves onto the integer: round(u) in [1, n - 2].  A u below 0.5
+// truncates to 0 or below (or saturates at INT_MIN), one past the top to n - 1 or above (or
+// INT_MAX), and NaN converts to 0: every one of them fails the test, as it fails on u.
 __device__ __forceinline__ unsigned sdf_cell(const DevModel& m, const double* __restrict__ p, bool& ok)
 {
-    const double ux = (p[0] - m.ox) * m.inv_res;
-    const double uy = (p[1] - m.oy) * m.inv_res;
-    const double uz = (p[2] - m.oz) * m.inv_res;
-    ok = ux >= 0.5 && uy >= 0.5 && uz >= 0.5 && ux < m.hi_x && uy < m.hi_y && uz < m.hi_z;
-    const double cell = (floor(ux + 0.5) * m.ny_d + floor(uy + 0.5)) * m.nz_d + floor(uz + 0.5);
-    return (unsigned)(ok ? cell : 0.0);
+    const int ix = (int)((p[0] - m.ox) * m.inv_res + 0.5);
+    const int iy = (int)((p[1] - m.oy) * m.inv_res + 0.5);
+    const int iz = (int)((p[2] - m.oz) * m.inv_res + 0.5);
+    ok = ix >= 1 && iy >= 1 && iz >= 1 && ix <= m.nx - 2 && iy <= m.ny - 2 && iz <= m.nz - 2;
+    const unsigned cell = ((unsigned)ix * (unsigned)m.ny + (unsigned)iy) * (unsigned)m.nz + (unsigned)iz;
+    return ok ? cell : 0u;
 }
 
 // Returns the voxel's squared cell distance d2 (0 outside: distance 0).
