@@ -381,7 +381,8 @@ def main():
 
     S = len(p.spheres)
     K_loc = e.K_loc
-    # per (rollout, waypoint) unit, one fp32 SDF voxel per sphere (4 S), the
+    # per (rollout, waypoint) unit, one fp32 SDF voxel per sphere (4 S; SURVEY's
+    # figure, kept for comparison across rounds: this field's voxel is 2 bytes), the
     # write + read of the fp64 noise per joint (16 J) and the fp64 state cost (8); one k_rollout
     # launch executes the K_loc noisy rollouts of this rank and the deferred noiseless one
     unit_bytes = 4 * S + 16 * p.J + 8
@@ -406,6 +407,10 @@ def main():
                     "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3),
                     "frac_vs_measured_6290": round(achieved / 6290.0, 5),
                     "sdf_only_gbs": round(rows_launch * p.N * 4 * S / avg_s / 1e9, 2),
+                    # this field's voxel is the 2-byte squared cell distance, not SURVEY's fp32
+                    "unit_bytes_actual": 2 * S + 16 * p.J + 8,
+                    "frac_actual_bytes": round(rows_launch * p.N * (2 * S + 16 * p.J + 8) / avg_s / 1e9 /
+                                               HBM_PEAK_GBS, 5),
                     "frac_rows_written_24J": round(bytes_written_rows / avg_s / 1e9 / HBM_PEAK_GBS, 5),
                     "iteration_bytes": (K - args.reused + 1) * p.N * unit_bytes,
                     "iteration_frac": round((K - args.reused + 1) * p.N * unit_bytes * value /

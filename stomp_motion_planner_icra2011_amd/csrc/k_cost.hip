@@ -181,7 +181,12 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
     // the pregen row's first chunk goes out with the image loads (one memory latency for both)
     PreChunk pc0;
-    if (pre) pre_chunk_load<BLOCK>(a.nz, e, 0, tid, pc0);
+    // a row priced by its pregen block (ctl_by_pre) needs no M eps here
+    const bool priced = !PHASED && a.ctl_by_pre;
+    if (pre) {
+        if (priced) pre_chunk_load<BLOCK, false>(a.nz, e, 0, tid, pc0);
+        else pre_chunk_load<BLOCK>(a.nz, e, 0, tid, pc0);
+    }
     if (gen) {
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
     } else if (!pre) {
@@ -224,7 +229,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     } else if (pre) {
         // the control costs are left to the pregen block of this row (ctl_by_pre) or, in the
         // phased body, to the FK-idle waves (defer)
-        if (defer || (!PHASED && a.ctl_by_pre)) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
+        if (priced) rollout_from_pre<BLOCK, true, false>(a.nz, e, traj, zA, zB, tid, pc0);
+        else if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
         else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid, pc0);
     }
     if (tid == 0) flag = 0;

@@ -527,7 +527,8 @@ struct PreChunk {
     double e[4], mp[4], th[4];
 };
 
-template <int BLOCK>
+// MP: also M eps (not needed when the row is priced elsewhere)
+template <int BLOCK, bool MP = true>
 __device__ __forceinline__ void pre_chunk_load(const NoiseArgs& a, int r, int idx0, int tid, PreChunk& c)
 {
     const int JN = a.J * a.N;
@@ -536,7 +537,7 @@ __device__ __forceinline__ void pre_chunk_load(const NoiseArgs& a, int r, int id
     for (int u = 0; u < 4; ++u) {
         const int idx = min(idx0 + tid + u * BLOCK, JN - 1);
         c.e[u] = a.pre_eps[row + idx];
-        c.mp[u] = a.pre_meps[row + idx];
+        if (MP) c.mp[u] = a.pre_meps[row + idx];
         c.th[u] = a.theta[idx];
     }
 }
@@ -544,7 +545,8 @@ __device__ __forceinline__ void pre_chunk_load(const NoiseArgs& a, int r, int id
 // the rollout kernel's row from k_pregen's eps and M eps: params = theta + eps into traj (LDS)
 // and HBM, the noise row, x = params + M eps, then the control costs (rollout_control).  first:
 // chunk 0, loaded by the caller (its loads in flight with the table image's)
-template <int BLOCK, bool DEFER = false>
+// XS = false: the row is priced by another workgroup (ctl_by_pre): no x, no M eps
+template <int BLOCK, bool DEFER = false, bool XS = true>
 __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
                                                  int tid, const PreChunk& first)
 {
@@ -554,7 +556,7 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
     for (int idx0 = 0; idx0 < JN; idx0 += 4 * BLOCK) {
         PreChunk c;
         if (idx0 == 0) c = first;
-        else pre_chunk_load<BLOCK>(a, r, idx0, tid, c);
+        else pre_chunk_load<BLOCK, XS>(a, r, idx0, tid, c);
         const double* e = c.e;
         const double* mp = c.mp;
         const double* th = c.th;
@@ -571,11 +573,11 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
                 } else if (r == 0) {
                     a.theta_gen[idx] = th[u];
                 }
-                xs[d * Nall + i + 6] = p + mp[u];
+                if (XS) xs[d * Nall + i + 6] = p + mp[u];
             }
         }
     }
-    if (!DEFER) rollout_control<BLOCK>(a, row, xs, zB, tid);
+    if (XS && !DEFER) rollout_control<BLOCK>(a, row, xs, zB, tid);
 }
 
 // computeControlCosts of row r from k_pregen's eps and M eps (covariant_trajectory_policy.cpp:
