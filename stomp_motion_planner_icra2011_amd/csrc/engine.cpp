@@ -94,6 +94,11 @@ struct stomp_engine {
     int J = 0, N = 0, Nall = 0, K = 0, Kr = 0, K_loc = 0, first = 0, S = 0, nseg = 0;
     int world = 1, rank = 0;
     bool split_modes = false;   // weights in the MINMAX / PSUM / USUM phases (world > 1, or the debug hook)
+    // gather mode (world > 1, small K N): every rank makes and prices the noise rows of all K rollouts
+    // (counter-based, so no noise moves), evaluates its own K_loc, and one all-gather of the state-cost
+    // rows per iteration gives every rank the whole cost matrix for the fused weights and the update
+    bool gather = false;
+    int rows = 0, row0 = 0;   // rollout rows held per iteration (K_loc, or K in gather mode); own rows' offset
     uint64_t seed = 0;
     double disc = 0.05, w_smooth = 0, w_obs = 0, w_con = 0, w_tq = 0;
     double smooth[3] = {0, 0, 0};
@@ -483,7 +488,7 @@ void launch_noiseless(stomp_engine* e, int member)
 void materialize_rows(stomp_engine* e)
 {
     if (!e->rows_in_pre) return;
-    launch_materialize_rows(e->K_loc, e->J * e->N, e->rows_eps, e->d_theta_gen, e->d_noise, e->d_params, e->stream);
+    launch_materialize_rows(e->rows, e->J * e->N, e->rows_eps, e->d_theta_gen, e->d_noise, e->d_params, e->stream);
     e->rows_in_pre = false;
 }
 
@@ -522,7 +527,9 @@ int local_gather(stomp_engine* e, const double* send, double* recv, size_t n)
     lk.unlock();
     for (int q = 0; q < g.world; ++q) {
         if (q != e->rank) HIP_TRY(e, hipStreamWaitEvent(e->stream, sl[q].ready, 0));
-        HIP_TRY(e, hipMemcpyAsync(recv + (size_t)q * n, sl[q].src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
+        if (recv + (size_t)q * n != sl[q].src)   // in place (gather mode: the rank's own rows)
+            HIP_TRY(e, hipMemcpyAsync(recv + (size_t)q * n, sl[q].src, n * sizeof(double), hipMemcpyDeviceToDevice,
+                                      e->stream));
     }
     HIP_TRY(e, hipEventRecord(e->ev_done, e->stream));
     lk.lock();
@@ -551,7 +558,7 @@ int exchange_max(stomp_engine* e, double* buf, size_t n)
     return 0;
 }
 
-// all-gather of n doubles per rank into recv [world][n]
+// all-gather of n doubles per rank into recv [world][n] (send may be recv's own slot: in place)
 int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
 {
 #ifdef STOMP_WITH_RCCL
@@ -561,8 +568,17 @@ int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
     }
 #endif
     if (e->local) return local_gather(e, send, recv, n);
-    HIP_TRY(e, hipMemcpyAsync(recv, send, sizeof(double) * n, hipMemcpyDeviceToDevice, e->stream));
+    if (recv != send) HIP_TRY(e, hipMemcpyAsync(recv, send, sizeof(double) * n, hipMemcpyDeviceToDevice, e->stream));
     return 0;
+}
+
+// gather mode: every rank's state-cost rows into every rank's [K][N] state buffer (in place;
+// with one rank, the STOMP_DEBUG_GATHER_RANKS timing hook, nothing moves)
+int exchange_state(stomp_engine* e)
+{
+    if (e->world == 1) return 0;
+    const size_t n = (size_t)e->K_loc * e->N;
+    return exchange_gather(e, e->d_state + (size_t)e->row0 * e->N, e->d_state, n);
 }
 
 // generateRollouts' sampling arguments of iteration it (policy_improvement_loop.cpp:155-160:
@@ -570,7 +586,8 @@ int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
 NoiseArgs noise_args(const stomp_engine* e, int it)
 {
     NoiseArgs na{};
-    na.J = e->J; na.N = e->N; na.Nall = e->Nall; na.K_loc = e->K_loc; na.first_global = e->first;
+    // gather mode: the noise rows of all K rollouts (global ids from 0)
+    na.J = e->J; na.N = e->N; na.Nall = e->Nall; na.K_loc = e->rows; na.first_global = e->first - e->row0;
     na.iteration = it; na.seed = e->seed;
     for (int d = 0; d < e->J; ++d) na.sigma.v[d] = e->sig_std[d] * std::pow(e->sig_dec[d], it - 1);
     na.theta = e->d_theta; na.LT = e->d_LT; na.MT = e->d_MT; na.start = e->d_start; na.goal = e->d_goal;
@@ -686,9 +703,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     // itself (fused), k_noise only projects and prices the reused rows after them
     const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
     const int num_gen = std::max(g1 - g0, 0);
-    if (fused) na.row_begin = num_gen;
+    if (fused) na.row_begin = e->gather ? e->rows : num_gen;
     // every local row generated (K_r = 0): eps and M eps come from k_pregen
     const bool pre = fused && e->pre_on && num_gen == e->K_loc;
+    if (e->gather && !(pre && e->pre_host == 1)) return fail(e, STOMP_E_INVALID, "gather mode needs the pregen rows");
     // outside the optimize loop the rows stay in the pregen buffer: the weights read eps there
     // and nothing else needs the noise / params rows on the device (reuse is off with pregen).
     // The optimize loop keeps the copies: after its stop the pregen blocks of the iterations
@@ -699,7 +717,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     if (pre) {
         if (e->pre_it != it) {   // not made ahead by the previous iteration's launches
             Timed tm(e, T_PREGEN);
-            launch_pregen(pregen_args(e, it), e->K_loc, e->stream);
+            launch_pregen(pregen_args(e, it), e->rows, e->stream);
         }
         e->pre_it = -1;
     }
@@ -716,9 +734,12 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
         if (pre && e->pre_host == 1) {
-            ca.pre_rows = e->K_loc;
+            ca.pre_rows = e->rows;
             ca.pre_next = pregen_args(e, it + 1);
-            ca.ctl_by_pre = ca.pre_rows >= ca.num_noisy ? 1 : 0;
+            ca.ctl_by_pre = 1;
+            ca.ctl_rows = e->rows;
+            ca.row0 = e->row0;
+            ca.state_out = e->d_state + (size_t)e->row0 * e->N;
             e->pre_it = it + 1;
         }
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
@@ -741,6 +762,8 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         // iteration's noiseless rollout leaves theta where the reference leaves it
         track_noiseless(e, ca);
     }
+    if (e->gather)
+        if (int rc = exchange_state(e)) return rc;
     if (reuse_late) {
         // the previous rows and the extra rollout (evaluated just now) ranked; the reused rows'
         // projection and control costs after them
@@ -752,10 +775,10 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     }
     WeightArgs wa{};
     wa.stop = e->d_stop;
-    wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
+    wa.J = e->J; wa.N = e->N; wa.K_loc = e->rows; wa.use_cumulative = e->use_cum;
     wa.state = e->d_state; wa.control = e->d_control; wa.noise = rows_pre ? na.pre_eps : e->d_noise;
     wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
-    wa.tc = weights_tile(e->K_loc);
+    wa.tc = weights_tile(e->rows);
     wa.nb_total = e->K / kSumBlock;
     wa.mm = e->d_mm; wa.psum_part = e->d_psum_part; wa.psum_all = e->d_psum_all; wa.u_part = e->d_u_part;
     // the first weights launch carries the next iteration's pregen rows
@@ -918,17 +941,49 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     e->J = d->num_joints; e->N = d->num_time_steps; e->Nall = e->N + 2 * kPad;
     e->K = d->num_rollouts; e->Kr = d->num_reused_rollouts;
     e->world = world; e->rank = world > 1 ? d->rank : 0;
-    // STOMP_DEBUG_SHARDED_MODES=1: a one-device engine runs the multi-GPU weights phases
-    // (test hook for the MINMAX / PSUM / USUM kernels; needs whole 64-rollout blocks, no reuse)
-    {
-        const char* dbg = std::getenv("STOMP_DEBUG_SHARDED_MODES");
-        e->split_modes = world > 1 || (dbg && dbg[0] == '1' && d->num_rollouts % kSumBlock == 0 &&
-                                       d->num_reused_rollouts == 0);
-    }
     e->K_loc = e->K / world; e->first = e->rank * e->K_loc;
     if (e->K_loc > kSumBlock * 64) {
         rc = fail(e, STOMP_E_INVALID, "at most %d rollouts per device", kSumBlock * 64);
         g_last_error = e->err; release(e); delete e; return rc;
+    }
+    {
+        // STOMP_PREGEN=0: the rollout kernel draws its own noise (A/B hook)
+        const char* pg = std::getenv("STOMP_PREGEN");
+#ifndef STOMP_SEPARATE_NOISE
+        const char* ph = std::getenv("STOMP_PREGEN_HOST");
+        e->pre_host = (ph && std::strcmp(ph, "weights") == 0) ? 2 : 1;
+        e->pre_on = e->Kr == 0 && e->J <= 16 && (e->pre_host == 1 || weights_carry_pregen(e->K_loc)) &&
+                    !(pg && pg[0] == '0');
+#endif
+    }
+    {
+        // the K-sharded decomposition.  gather: one all-gather of the state-cost rows
+        // per iteration, every rank making and pricing all K noise rows; partials: three exchanges
+        // of 64-rollout block partials (MINMAX / PSUM / USUM weights phases).  Default: gather while
+        // the state rows of all K rollouts are at most 1 MiB (cfg2: 396 KB; cfg3's 6.5 MB stay
+        // partials), STOMP_SHARD_MODE=gather|partials to choose.  Gather needs the pregen rows in
+        // the rollout launch and no reuse.
+        const bool can = e->pre_on && e->pre_host == 1 && e->Kr == 0 && e->K <= kSumBlock * 64;
+        const char* sm = std::getenv("STOMP_SHARD_MODE");
+        // STOMP_DEBUG_GATHER_RANKS=W: a one-device engine times rank 0 of W gather-mode ranks (its
+        // K / W rollouts, all K rows made and weighted; nothing exchanged, so results are not the
+        // sharded ones: a timing hook)
+        const char* sim = std::getenv("STOMP_DEBUG_GATHER_RANKS");
+        const int W = (world == 1 && sim) ? std::atoi(sim) : 0;
+        if (W > 1 && can && e->K % (W * kSumBlock) == 0) {
+            e->gather = true;
+            e->K_loc = e->K / W;
+        } else if (world > 1 && can) {
+            e->gather = sm ? std::strcmp(sm, "gather") == 0 : (size_t)e->K * e->N * sizeof(double) <= (1u << 20);
+        }
+        e->rows = e->gather ? e->K : e->K_loc;
+        e->row0 = (e->gather && world > 1) ? e->first : 0;
+        // STOMP_DEBUG_SHARDED_MODES=1: a one-device engine runs the multi-GPU weights phases
+        // (test hook for the MINMAX / PSUM / USUM kernels; needs whole 64-rollout blocks, no reuse)
+        const char* dbg = std::getenv("STOMP_DEBUG_SHARDED_MODES");
+        e->split_modes = (world > 1 && !e->gather) ||
+                         (world == 1 && !e->gather && dbg && dbg[0] == '1' && d->num_rollouts % kSumBlock == 0 &&
+                          d->num_reused_rollouts == 0);
     }
     e->S = d->num_spheres; e->nseg = d->num_segments; e->seed = d->seed;
     e->disc = d->discretization; e->w_smooth = d->smoothness_cost_weight; e->w_obs = d->obstacle_cost_weight;
@@ -1020,12 +1075,14 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     } else {
         CREATE_TRY(upload(e, &e->d_sdf, d->grid.data, ncell));
     }
-    const size_t KJN = (size_t)e->K_loc * J * N;
+    const size_t KJN = (size_t)e->rows * J * N;
     CREATE_TRY(dev_alloc(e, &e->d_params, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_noise, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_control, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_prob, KJN));
-    CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->K_loc * N));
+    CREATE_TRY(dev_alloc(e, &e->d_state, (size_t)e->rows * N));
+    if (e->gather && hipMemsetAsync(e->d_state, 0, sizeof(double) * e->rows * N, e->stream) != hipSuccess)
+        CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     if (e->Kr > 0) {
         CREATE_TRY(dev_alloc(e, &e->d_params_b, KJN));
         CREATE_TRY(dev_alloc(e, &e->d_noise_b, KJN));
@@ -1041,16 +1098,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(dev_alloc(e, &e->d_psum_all, nb_tot * J * N));
         CREATE_TRY(dev_alloc(e, &e->d_u_part, nb_loc * J * N));
         CREATE_TRY(dev_alloc(e, &e->d_u_all, nb_tot * J * N));
-    }
-    {
-        // STOMP_PREGEN=0: the rollout kernel draws its own noise (A/B hook)
-        const char* pg = std::getenv("STOMP_PREGEN");
-#ifndef STOMP_SEPARATE_NOISE
-        const char* ph = std::getenv("STOMP_PREGEN_HOST");
-        e->pre_host = (ph && std::strcmp(ph, "weights") == 0) ? 2 : 1;
-        e->pre_on = e->Kr == 0 && J <= 16 && (e->pre_host == 1 || weights_carry_pregen(e->K_loc)) &&
-                    !(pg && pg[0] == '0');
-#endif
     }
     if (e->pre_on)
         for (int b = 0; b < 2; ++b) {
@@ -1163,7 +1210,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
                 CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "state-terms kernel needs %zu B of LDS", terms_lds_bytes(t)));
             e->torque_stats = false;
         }
-        if (e->terms_on) CREATE_TRY(dev_alloc(e, &e->d_terms_traj, KJN));
+        if (e->terms_on) CREATE_TRY(dev_alloc(e, &e->d_terms_traj, (size_t)e->K_loc * J * N));
         if (e->torque_stats) {
             e->tq_model = t;
             e->tq_model.torque = 1;
@@ -1570,7 +1617,7 @@ int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* nois
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
     materialize_rows(e);
-    if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
+    if (e->world > 1 || e->gather) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
     if (!noise_stddev) return fail(e, STOMP_E_INVALID, "null noise_stddev");
     flush_noiseless(e);
     if (int rc = begin_generate(e)) return rc;
@@ -1639,7 +1686,7 @@ int stomp_pi_improve_policy(stomp_engine* e, double* updates)
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
     materialize_rows(e);
-    if (e->world > 1) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
+    if (e->world > 1 || e->gather) return fail(e, STOMP_E_UNSUPPORTED, "the PolicyImprovement API is single-rank");
     WeightArgs wa{};
     wa.stop = nullptr;
     wa.J = e->J; wa.N = e->N; wa.K_loc = e->K_loc; wa.use_cumulative = e->use_cum;
@@ -1730,15 +1777,16 @@ int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
 {
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
-    const size_t KJN = (size_t)e->K_loc * e->J * e->N;
+    // this rank's rows (gather mode holds all K: its own start at row0)
+    const size_t JN = (size_t)e->J * e->N, KJN = (size_t)e->K_loc * JN, o = (size_t)e->row0 * JN;
     const double* src = nullptr;
     size_t n = KJN;
     if (!std::strcmp(which, "params") || !std::strcmp(which, "noise")) materialize_rows(e);
-    if (!std::strcmp(which, "params")) src = e->d_params;
-    else if (!std::strcmp(which, "noise")) src = e->d_noise;
-    else if (!std::strcmp(which, "control_costs")) src = e->d_control;
-    else if (!std::strcmp(which, "probabilities")) src = e->d_prob;
-    else if (!std::strcmp(which, "state_costs")) { src = e->d_state; n = (size_t)e->K_loc * e->N; }
+    if (!std::strcmp(which, "params")) src = e->d_params + o;
+    else if (!std::strcmp(which, "noise")) src = e->d_noise + o;
+    else if (!std::strcmp(which, "control_costs")) src = e->d_control + o;
+    else if (!std::strcmp(which, "probabilities")) src = e->d_prob + o;
+    else if (!std::strcmp(which, "state_costs")) { src = e->d_state + (size_t)e->row0 * e->N; n = (size_t)e->K_loc * e->N; }
     else if (!std::strncmp(which, "x_", 2)) {
         // the extra (noiseless) rollout of addExtraRollouts (policy_improvement.cpp:443-462);
         // x_state_costs is written by every noiseless rollout, the others only with reuse
@@ -2313,7 +2361,7 @@ int stomp_group_create(stomp_engine* const* engines, int32_t n, stomp_group** ou
             rollout_lds_bytes(e->model, e->model.pad_lds) != lds0)
             return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model)");
         if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->pre_host != 1 || e->terms_on ||
-            e->split_modes || e->use_cum || e->J > 16)
+            e->split_modes || e->gather || e->use_cum || e->J > 16)
             return gfail(nullptr, STOMP_E_UNSUPPORTED,
                          "groups run single-device engines without reuse, state-cost terms or cumulative costs");
     }
@@ -2402,6 +2450,7 @@ int stomp_group_run(stomp_group* g, int32_t first, int32_t count)
             ca.pre_rows = e->K_loc;
             ca.pre_next = pregen_args(e, it + 1);
             ca.ctl_by_pre = 1;
+            ca.ctl_rows = e->K_loc;
             e->pre_it = it + 1;
             if (e->pending_member >= 0) {
                 ca.x_params = e->d_theta; ca.x_member = e->pending_member;

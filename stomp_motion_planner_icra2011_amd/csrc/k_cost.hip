@@ -130,7 +130,9 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double* pA = (double*)(lds_raw + L.nzA);
             double* pB = (double*)(lds_raw + L.nzB);
             const int r = bid - nro;
-            if (!PHASED && a.ctl_by_pre && r < a.num_noisy && !(a.stop && *a.stop)) {
+            // a phased launch's rollouts price their own rows (the FK-idle waves)
+            const bool own = PHASED && r >= a.row0 && r < a.row0 + a.num_noisy;
+            if (a.ctl_by_pre && r < a.ctl_rows && !own && !(a.stop && *a.stop)) {
                 // this iteration's row r priced here instead of on its rollout's critical path
                 pre_row_control<BLOCK>(a.nz, r, pA, pB, threadIdx.x);
                 __syncthreads();   // pA / pB are the normals' buffers next
@@ -183,9 +185,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     PreChunk pc0;
     // a row priced by its pregen block (ctl_by_pre) needs no M eps here
     const bool priced = !PHASED && a.ctl_by_pre;
+    const int pr = e + a.row0;   // the row in the pregen buffers
     if (pre) {
-        if (priced) pre_chunk_load<BLOCK, false>(a.nz, e, 0, tid, pc0);
-        else pre_chunk_load<BLOCK>(a.nz, e, 0, tid, pc0);
+        if (priced) pre_chunk_load<BLOCK, false>(a.nz, pr, 0, tid, pc0);
+        else pre_chunk_load<BLOCK>(a.nz, pr, 0, tid, pc0);
     }
     if (gen) {
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
@@ -229,9 +232,9 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     } else if (pre) {
         // the control costs are left to the pregen block of this row (ctl_by_pre) or, in the
         // phased body, to the FK-idle waves (defer)
-        if (priced) rollout_from_pre<BLOCK, true, false>(a.nz, e, traj, zA, zB, tid, pc0);
-        else if (defer) rollout_from_pre<BLOCK, true>(a.nz, e, traj, zA, zB, tid, pc0);
-        else rollout_from_pre<BLOCK>(a.nz, e, traj, zA, zB, tid, pc0);
+        if (priced) rollout_from_pre<BLOCK, true, false>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
+        else if (defer) rollout_from_pre<BLOCK, true>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
+        else rollout_from_pre<BLOCK>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
     }
     if (tid == 0) flag = 0;
     __syncthreads();
@@ -435,7 +438,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             const int nfk = fk_w1 - fk_w0 + 1;
             const int cw = wv < fk_w0 ? wv : wv - nfk;
             for (int d = cw; d < J; d += NW - nfk)
-                wave_control(a.nz, (size_t)e * J * N, zA, zB, d, lane);
+                wave_control(a.nz, (size_t)pr * J * N, zA, zB, d, lane);
         }
         if (fk_lane) {
             for (int op = 0; op < m.nops; ++op) {

@@ -189,9 +189,13 @@ struct CostArgs {
     int x_member;
     int pre_rows;               // > 0: blocks after the rollouts make k_pregen's rows of pre_next (the
     NoiseArgs pre_next;         // next iteration) at low priority in the same dispatch
-    int ctl_by_pre;             // with fused_noise 2 and pre_rows >= num_noisy: pregen block r also prices
-                                // this iteration's row r (computeControlCosts, off the rollout's
-                                // critical path); the rollout workgroups skip it
+    int ctl_by_pre;             // with fused_noise 2 and pre_rows >= ctl_rows: pregen block r < ctl_rows also
+                                // prices this iteration's row r (computeControlCosts, off the rollout's
+                                // critical path) and writes its noise / params rows; the (slot-loop)
+                                // rollout workgroups skip both (phased ones price their own rows)
+    int ctl_rows;               // rows priced by the pregen blocks (num_noisy; all K of a gather-mode rank)
+    int row0;                   // rollout e's row in nz's row buffers is row0 + e (gather mode: the
+                                // rank's first global rollout; its state goes to state_out[e])
     double* x_state;
     uint8_t* x_cf;
     double* x_traj;

@@ -545,10 +545,11 @@ __device__ __forceinline__ void pre_chunk_load(const NoiseArgs& a, int r, int id
 // the rollout kernel's row from k_pregen's eps and M eps: params = theta + eps into traj (LDS)
 // and HBM, the noise row, x = params + M eps, then the control costs (rollout_control).  first:
 // chunk 0, loaded by the caller (its loads in flight with the table image's)
-// XS = false: the row is priced by another workgroup (ctl_by_pre): no x, no M eps
+// XS = false: the row is priced by another workgroup (ctl_by_pre), which also writes its noise /
+// params rows: no x, no M eps, no row stores.  lead: the launch's first rollout (keeps theta_gen)
 template <int BLOCK, bool DEFER = false, bool XS = true>
-__device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
-                                                 int tid, const PreChunk& first)
+__device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, bool lead, double* traj, double* zA,
+                                                 double* zB, int tid, const PreChunk& first)
 {
     const int J = a.J, N = a.N, Nall = a.Nall, JN = J * N;
     const size_t row = (size_t)r * JN;
@@ -568,9 +569,11 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
                 const double p = th[u] + e[u];
                 traj[idx] = p;
                 if (!a.rows_in_pre) {
-                    a.noise[row + idx] = e[u];
-                    a.params[row + idx] = p;
-                } else if (r == 0) {
+                    if (XS) {
+                        a.noise[row + idx] = e[u];
+                        a.params[row + idx] = p;
+                    }
+                } else if (lead) {
                     a.theta_gen[idx] = th[u];
                 }
                 if (XS) xs[d * Nall + i + 6] = p + mp[u];
@@ -582,8 +585,9 @@ __device__ __forceinline__ void rollout_from_pre(const NoiseArgs& a, int r, doub
 
 // computeControlCosts of row r from k_pregen's eps and M eps (covariant_trajectory_policy.cpp:
 // 228-255 via policy_improvement.cpp:292-299): x = (theta + eps) + M eps, the expressions of
-// rollout_from_pre, then rollout_control into a.control.  Run by the rollout launch's pregen block
-// r, so the rollout workgroup of row r leaves the pricing out of its critical path.
+// rollout_from_pre, then rollout_control into a.control; the noise / params rows too unless they
+// stay in the pregen buffer.  Run by the rollout launch's pregen block r, so the rollout workgroup
+// of row r leaves the pricing out of its critical path.
 template <int BLOCK>
 __device__ __forceinline__ void pre_row_control(const NoiseArgs& a, int r, double* xs, double* cs, int tid)
 {
@@ -598,6 +602,10 @@ __device__ __forceinline__ void pre_row_control(const NoiseArgs& a, int r, doubl
                 const int d = idx / N, i = idx - d * N;
                 const double p = c.th[u] + c.e[u];
                 xs[d * Nall + i + 6] = p + c.mp[u];
+                if (!a.rows_in_pre) {
+                    a.noise[(size_t)r * JN + idx] = c.e[u];
+                    a.params[(size_t)r * JN + idx] = p;
+                }
             }
         }
     }

@@ -1,10 +1,14 @@
 """The engine's rank > 0 code path, on one GPU.
 
 The K-sharded multi-GPU iteration: rank r owns global rollouts
-[r K/W, (r+1) K/W) (first_global, K_loc), generates exactly those rows of the counter-based
-noise, and the ranks exchange (1) all-reduce(max) of [max S, -min S], (2) all-gather of the
-per-64-rollout-block exp sums, (3) all-gather of the per-block eps * P sums, then apply
-delta theta = M u redundantly (policy_improvement.cpp:322-383).  Here the W ranks are W engines
+[r K/W, (r+1) K/W) (first_global, K_loc).  Two decompositions:
+  partials: each rank generates exactly its rows of the counter-based noise, and the ranks
+    exchange (1) all-reduce(max) of [max S, -min S], (2) all-gather of the per-64-rollout-block
+    exp sums, (3) all-gather of the per-block eps * P sums;
+  gather (STOMP_SHARD_MODE=gather, K_r = 0): every rank makes and prices the noise rows of all K
+    rollouts, evaluates its own, and one all-gather of the state-cost rows gives every rank the
+    whole cost matrix;
+then every rank applies delta theta = M u redundantly (policy_improvement.cpp:322-383).  Here the W ranks are W engines
 of one process on device 0, each driven by its own host thread, exchanging through the
 engine's in-process group (stomp_comm_local_id: device copies ordered by HIP events, in place
 of RCCL).  Every rank must reproduce its slice of the single-process oracle BIT FOR BIT:
@@ -24,7 +28,12 @@ pytestmark = pytest.mark.gpu
 THREADS = int(os.environ.get("OMP_NUM_THREADS") or 8)
 
 
-def make_ranks(p, world):
+MODES = ["partials", "gather"]
+
+
+def make_ranks(p, world, mode=None, monkeypatch=None):
+    if mode is not None:
+        monkeypatch.setenv("STOMP_SHARD_MODE", mode)
     gid = eng.comm_local_id(world)
     return [eng.Engine(p, rank=r, world_size=world, comm_id=gid) for r in range(world)]
 
@@ -35,13 +44,15 @@ def on_threads(engines, fn):
         return [f.result(timeout=300) for f in futs]
 
 
-@pytest.mark.parametrize("world,K,Kr", [(2, 256, 0), (4, 256, 0), (2, 128, 64), (4, 256, 90), (8, 512, 200)])
-def test_ranks_iterate_bitwise(world, K, Kr):
+@pytest.mark.parametrize("world,K,Kr,mode", [(2, 256, 0, "partials"), (4, 256, 0, "partials"), (2, 256, 0, "gather"),
+                                             (4, 256, 0, "gather"), (2, 128, 64, None), (4, 256, 90, None),
+                                             (8, 512, 200, None)])
+def test_ranks_iterate_bitwise(world, K, Kr, mode, monkeypatch):
     """Kr > 0: the reuse ranking over all ranks' rows (all-gathered totals), the chosen rows moved
     to their destination shard (policy_improvement.cpp:176-225); 90 and 200 reused rows straddle
-    shard boundaries"""
+    shard boundaries (partials: gather mode needs K_r = 0)"""
     p = pb.make_problem(grid_n=64, num_rollouts=K, num_reused_rollouts=Kr)
-    engines = make_ranks(p, world)
+    engines = make_ranks(p, world, mode, monkeypatch)
     K_loc = K // world
     for r, e in enumerate(engines):
         assert (e.first, e.K_loc) == (r * K_loc, K_loc)
@@ -72,11 +83,12 @@ def test_ranks_iterate_bitwise(world, K, Kr):
         e.close()
 
 
-def test_eight_ranks_cfg2_strong_scaling_shape():
+@pytest.mark.parametrize("mode", MODES)
+def test_eight_ranks_cfg2_strong_scaling_shape(mode, monkeypatch):
     # the 8-GPU decomposition of the headline config: K = 512 over 8 ranks (64 rollouts, one
     # block each), enqueued by run() with no host sync inside the chunk
     p = pb.make_problem(grid_n=128, num_rollouts=512, num_reused_rollouts=0)
-    engines = make_ranks(p, 8)
+    engines = make_ranks(p, 8, mode, monkeypatch)
     o = po.Oracle(p, threads=THREADS)
 
     def drive(r, e):
@@ -102,13 +114,14 @@ def test_eight_ranks_cfg2_strong_scaling_shape():
         e.close()
 
 
-@pytest.mark.parametrize("Kr,after_cf", [(0, 1000), (64, 1000), (40, 3)])
-def test_ranks_optimize_loop(Kr, after_cf):
+@pytest.mark.parametrize("Kr,after_cf,mode", [(0, 1000, "partials"), (0, 1000, "gather"), (0, 3, "gather"),
+                                              (64, 1000, None), (40, 3, None)])
+def test_ranks_optimize_loop(Kr, after_cf, mode, monkeypatch):
     # the device-resident optimize loop on every rank (identical stop decisions), with and
     # without reuse across the shards
     p = pb.make_problem(grid_n=64, num_rollouts=128, num_reused_rollouts=Kr, max_iterations=30,
                         max_iterations_after_collision_free=after_cf)
-    engines = make_ranks(p, 2)
+    engines = make_ranks(p, 2, mode, monkeypatch)
     o = po.Oracle(p, threads=THREADS)
     ost, ocosts = o.optimize()
 

@@ -115,6 +115,68 @@ def test_two_rank_reduction_is_bitwise_single_rank():
         np.testing.assert_array_equal(theta, ref["theta1"])
 
 
+# ---- gather mode (STOMP_SHARD_MODE=gather, engine.cpp exchange_state): every rank makes and prices
+# the noise rows of all K rollouts (counter-based noise: the full noise / control rows here stand
+# for that regeneration), evaluates only its own rows' state costs, and ONE all-gather of the
+# state-cost rows gives every rank the whole cost matrix; the weights and the update then run
+# exactly as on one device (canonical 64-rollout block order over all K).
+def _canonical_update(S, eps, M, theta0):
+    Kall, J, N = S.shape
+    mx, mn = S.max(axis=0), S.min(axis=0)
+    den = np.maximum(mx - mn, 1e-8)
+    E = np.empty_like(S)
+    for idx in np.ndindex(S.shape):
+        r, d, t = idx
+        E[idx] = po.dexp(-10.0 * (S[idx] - mn[d, t]) / den[d, t])
+    nb = Kall // B
+
+    def blocked(X):
+        return np.array([[_seq_sum(_seq_sum(X[b * B:(b + 1) * B, d, t]) for b in range(nb)) for t in range(N)]
+                         for d in range(J)])
+    P = E / blocked(E)[None]
+    u = blocked(eps * P)
+    theta = theta0.copy()
+    for d in range(J):
+        for i in range(N):
+            theta[d, i] += 1.0 * _seq_sum(M[i, k] * u[d, k] for k in range(N))
+    return P, theta
+
+
+def _gather_worker(rank, world, port, ref, out_q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    K_loc = K // world
+    r0 = rank * K_loc
+    own = torch.from_numpy(np.ascontiguousarray(ref["state"][r0:r0 + K_loc]))   # this rank's rollouts only
+    gathered = [torch.zeros_like(own) for _ in range(world)]
+    dist.all_gather(gathered, own)
+    state = torch.cat(gathered).numpy()                                          # [K][N], global row order
+    S = state[:, None, :] + ref["control"]
+    P, theta = _canonical_update(S, ref["noise"], ref["M"], ref["theta0"])
+    out_q.put((rank, P, theta))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_gather_mode_is_bitwise_single_rank():
+    ref = _reference()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, ref, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, P, theta in res:
+        np.testing.assert_array_equal(P, ref["prob"])
+        np.testing.assert_array_equal(theta, ref["theta1"])
+
+
 # ---- rollout reuse across ranks (K_r > 0; engine.cpp begin_generate, k_misc.hip k_reuse_*):
 # every rank prices its own rows (Rollout::getCost, policy_improvement.cpp:149-156), the totals
 # are all-gathered, every rank ranks all K + 1 candidates the way std::sort orders the
