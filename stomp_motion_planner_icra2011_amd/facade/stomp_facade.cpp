@@ -323,7 +323,9 @@ bool CovariantTrajectoryPolicy::loadDifferentiation()
 
 // costs_all += (weight * derivative_costs_[i]) * (D_i x)^2 for the three rules, x = parameters_all_[d]
 // with the free segment replaced (covariant_trajectory_policy.cpp:236-243, 285-291); the dense
-// row products run over the stencil's band (the other entries of D_i are exact zeros)
+// row products run over the stencil's band (the other entries of D_i are exact zeros), summed left
+// to right as in the engine and the oracle; Eigen's GEMV may order the sum differently (DESIGN.md 3,
+// parity unpinned there)
 void CovariantTrajectoryPolicy::accumulateCosts(int d, const VectorXd& free, const double weight,
                                                 VectorXd& costs_all) const
 {
