@@ -2449,8 +2449,10 @@ int stomp_group_run(stomp_group* g, int32_t first, int32_t count)
             ca.member = member; ca.state_out = e->d_state;
             ca.pre_rows = e->K_loc;
             ca.pre_next = pregen_args(e, it + 1);
-            ca.ctl_by_pre = 1;
-            ca.ctl_rows = e->K_loc;
+            // the grouped launch is throughput-bound: its rollout workgroups price their own rows
+            // (pricing in the pregen blocks re-reads theta and eps: cfg5 55.7k vs 53.9-54.5k
+            // problem-it/s)
+            ca.ctl_by_pre = 0;
             e->pre_it = it + 1;
             if (e->pending_member >= 0) {
                 ca.x_params = e->d_theta; ca.x_member = e->pending_member;

@@ -111,7 +111,11 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x)
 
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
-template <int BLOCK, bool PHASED = false>
+// FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
+// slot's gathers are in flight (the running frame then stays live across the pair phases); off,
+// they advance after the fold from the frame reloaded from fb (fewer live registers: the grouped
+// launch, which is throughput-bound and register-capped at three workgroups per CU)
+template <int BLOCK, bool PHASED = false, bool FK_OVERLAP = true>
 __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -581,6 +585,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             for (int k = 0; k < 12; ++k) F[k] = fb[k * N + pt];
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
+                if (u * G >= ns) break;   // uniform: no lane takes a u-th sphere of this run
                 const double* pos = sph[sb + min(pg + u * G, ns - 1)].pos;
                 double x[3];
 #pragma unroll
@@ -596,9 +601,12 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // while the gathers are in flight the FK lanes run the program on to the next sphere
         // segment (C in registers; fb keeps this slot's frame for the velocities, and the next
         // frame is published after the fold)
-        __builtin_amdgcn_s_setprio(3);
-        const int next_op = fk_advance(op + 1);
-        __builtin_amdgcn_s_setprio(2);
+        int next_op = op;
+        if constexpr (FK_OVERLAP) {
+            __builtin_amdgcn_s_setprio(3);
+            next_op = fk_advance(op + 1);
+            __builtin_amdgcn_s_setprio(2);
+        }
         if (pg < G) {
             // the potentials and the pair list
 #pragma unroll
@@ -639,6 +647,15 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
             av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
         }
+        if constexpr (!FK_OVERLAP) {
+            // C is reloaded from fb (not kept live across the pairs)
+            if (fk_lane) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
+            }
+        }
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
         __builtin_amdgcn_s_setprio(3);
@@ -658,7 +675,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             }
         }
         // the program's control flow is uniform, so every lane has the same next op
-        op = next_op;
+        if constexpr (FK_OVERLAP) op = next_op;
+        else op = fk_advance(op + 1);
         __builtin_amdgcn_s_setprio(2);
         STAMP(13 + 4 * run);
         ++run;
@@ -733,7 +751,7 @@ __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_g
         p = j / npre;
         bid = nro + (j - p * npre);
     }
-    rollout_body<BLOCK>(ms[p], as[p], bid);
+    rollout_body<BLOCK, false, false>(ms[p], as[p], bid);
 }
 
 STOMP_STAMP_ACCESSORS(cost)
