@@ -246,35 +246,32 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     BLOCK_MARK(4);
 
     // ---- handleJointLimits
-    int any = 0;
-    for (int idx = tid; idx < J * N; idx += BLOCK) {
-        const int j = idx / N;
-        if (!hl_s[j]) continue;
-        const double v = traj[idx], jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
-        double absamt = 0.0;
-        if (v > jmax) absamt = fabs(jmax - v);
-        else if (v < jmin) absamt = fabs(jmin - v);
-        any |= absamt > 1e-6;
-    }
     // Joints are independent: the limited joints are dealt round-robin over the waves and a wave
     // runs the passes of two of its joints in lockstep (pass p of one beside pass p of the other,
     // each joint still stopping on its own), so the two Q^-1 column loads of a step are in flight
     // together.  The argmax is a wave butterfly (every lane ends with the same (max, first
     // index)) and a pass needs no block barrier: LDS accesses of one wave execute in program order.
-    if (__syncthreads_or(any)) {
+    // A joint without violations costs its wave one argmax (no block-wide pre-scan: the barrier
+    // above already published traj).
+    {
         __builtin_amdgcn_s_setprio(3);   // a dependent chain per joint (critical path)
-        // the violated waypoint a pass of joint j corrects (wave-uniform), -1 when none is left
-        auto jl_argmax = [&](int j) -> int {
-            const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
-            const double* tj = traj + j * N;
+        // A wave keeps its joints' rows in registers through the passes (lane l: waypoints l,
+        // l + 64, ...; N <= 256), so a pass is the argmax, the column load and the update with
+        // no LDS round trip; the rows go back to traj after the last pass.
+        // the violated waypoint a pass corrects (wave-uniform), -1 when none is left
+        auto jl_argmax = [&](const double* v, double jmin, double jmax) -> int {
             double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
             int ci = 0;
-            for (int t = lane; t < N; t += 64) {
-                const double v = tj[t];
-                double absamt = 0.0;
-                if (v > jmax) absamt = fabs(jmax - v);
-                else if (v < jmin) absamt = fabs(jmin - v);
-                if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = lane + 64 * u;
+                if (t < N) {
+                    const double x = v[u];
+                    double absamt = 0.0;
+                    if (x > jmax) absamt = fabs(jmax - x);
+                    else if (x < jmin) absamt = fabs(jmin - x);
+                    if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
+                }
             }
             // wave argmax, first index on ties: the bits of a non-negative double order like
             // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
@@ -291,27 +288,43 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             }
             return cm;
         };
-        // traj_j += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
-        auto jl_apply = [&](int j, int cm, const double* qv, double qd) {
-            const double jmin = jlim_s[2 * j], jmax = jlim_s[2 * j + 1];
-            double* tj = traj + j * N;
-            const double v = tj[cm];
-            const double amount = v > jmax ? jmax - v : jmin - v;
+        // row += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
+        auto jl_apply = [&](double* v, int cm, double jmin, double jmax, const double* qv, double qd) {
+            double vu = v[0];
+#pragma unroll
+            for (int u = 1; u < 4; ++u)
+                if ((cm >> 6) == u) vu = v[u];   // uniform select
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
+            const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
+            const unsigned vhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), cm & 63);
+            const double x = __longlong_as_double((long long)(((unsigned long long)vhi << 32) | vlo));
+            const double amount = x > jmax ? jmax - x : jmin - x;
             const double mult = amount / qd;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (lane + 64 * u < N) tj[lane + 64 * u] += mult * qv[u];
+                if (lane + 64 * u < N) v[u] += mult * qv[u];
         };
         auto jl_pair = [&](int ja, int jb) {
-            bool la = true, lb = jb >= 0;
+            const bool hb = jb >= 0;
+            const int jb0 = hb ? jb : ja;
+            const double amin = jlim_s[2 * ja], amax = jlim_s[2 * ja + 1];
+            const double bmin = jlim_s[2 * jb0], bmax = jlim_s[2 * jb0 + 1];
+            double va[4], vb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = min(lane + 64 * u, N - 1);
+                va[u] = traj[ja * N + t];
+                vb[u] = traj[jb0 * N + t];
+            }
+            bool la = true, lb = hb;
             for (int pass = 0; pass < 11 && (la || lb); ++pass) {
                 int ca = -1, cb = -1;
-                if (la) { ca = jl_argmax(ja); la = ca >= 0; }
-                if (lb) { cb = jl_argmax(jb); lb = cb >= 0; }
+                if (la) { ca = jl_argmax(va, amin, amax); la = ca >= 0; }
+                if (lb) { cb = jl_argmax(vb, bmin, bmax); lb = cb >= 0; }
                 if (!la && !lb) break;
                 // both columns and diagonals in flight (unconditional loads, clamped; N <= 256)
                 const double* Qa = m.QT + ((size_t)ja * N + (size_t)max(ca, 0)) * N;
-                const double* Qb = m.QT + ((size_t)max(jb, 0) * N + (size_t)max(cb, 0)) * N;
+                const double* Qb = m.QT + ((size_t)jb0 * N + (size_t)max(cb, 0)) * N;
                 double qa[4], qb[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -319,9 +332,16 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                     qb[u] = Qb[min(lane + 64 * u, N - 1)];
                 }
                 const double qda = Qa[max(ca, 0)], qdb = Qb[max(cb, 0)];
-                if (la) jl_apply(ja, ca, qa, qda);
-                if (lb) jl_apply(jb, cb, qb, qdb);
-                __builtin_amdgcn_wave_barrier();
+                if (la) jl_apply(va, ca, amin, amax, qa, qda);
+                if (lb) jl_apply(vb, cb, bmin, bmax, qb, qdb);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = lane + 64 * u;
+                if (t < N) {
+                    traj[ja * N + t] = va[u];
+                    if (hb) traj[jb * N + t] = vb[u];
+                }
             }
         };
         int mine = -1, k = 0;
