@@ -135,3 +135,33 @@ def test_ranks_optimize_loop(Kr, after_cf, mode, monkeypatch):
         np.testing.assert_array_equal(best, o.best_trajectory())
     for e in engines:
         e.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_ranks_with_state_terms_bitwise(mode, monkeypatch):
+    # the state-cost terms (torque, orientation constraint; k_terms) on a rank's own rows: in
+    # gather mode they land at the rank's offset of the all-K state buffer before the all-gather
+    p = pb.make_problem(grid_n=64, num_rollouts=128, num_reused_rollouts=0, torque_cost_weight=0.001,
+                        orientation_constraints=[pb.upright_constraint()])
+    engines = make_ranks(p, 2, mode, monkeypatch)
+    o = po.Oracle(p, threads=THREADS)
+
+    def drive(r, e):
+        rec = []
+        for it in range(1, 4):
+            c = e.iterate(it)
+            rec.append((c, e.theta(), e.rollouts("state_costs"), e.rollouts("probabilities")))
+        return rec
+
+    recs = on_threads(engines, drive)
+    for k, it in enumerate(range(1, 4)):
+        oc = o.iterate(it)
+        st, pr = o.rollouts("state_costs"), o.rollouts("probabilities")
+        for r in range(2):
+            c, th, s, pp = recs[r][k]
+            assert c == oc, (it, r)
+            np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it} rank {r}")
+            np.testing.assert_array_equal(s, st[64 * r:64 * (r + 1)])
+            np.testing.assert_array_equal(pp, pr[64 * r:64 * (r + 1)])
+    for e in engines:
+        e.close()
