@@ -647,10 +647,11 @@ int run_reuse(stomp_engine* e)
     const int with_extra = e->extra_added ? 1 : 0;
     e->extra_added = false;
     if (e->world == 1) {
-        if (launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
+        if (int rc = launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
                          e->d_params, e->d_noise, e->d_state, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta,
                          e->d_stop, e->stream))
-            return fail(e, STOMP_E_INVALID, "reuse: the source and destination rollout rows alias");
+            return fail(e, STOMP_E_INVALID, rc == -1 ? "reuse: the source and destination rollout rows alias"
+                                                     : "reuse: the cost rows of one candidate exceed the LDS");
         return 0;
     }
     const size_t slot = (size_t)e->Kr * ((size_t)e->J * e->N + e->N);

@@ -155,22 +155,77 @@ __device__ __forceinline__ void reuse_totals_block(int c0, int c1, int K, int J,
 // K previous rollouts and the extra (noiseless) rollout by Rollout::getCost (:149-156),
 // lexicographic on (cost, index) with the extra rollout at index -1 (std::sort of pairs), copy
 // the best K_r into rows K_gen.. and re-base their noise on the current theta.
-__global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra,
-                                               const double* src_params, const double* src_state,
-                                               const double* control, double* params, double* noise, double* state,
-                                               const double* x_params, const double* x_state,
-                                               const double* x_control, const double* theta, const int* stop)
+// One 1024-lane workgroup, latency-bound throughout, so every phase puts all its loads in flight
+// at once: the candidates' cost rows (state row + J control rows, P = (J + 1) N doubles each) are
+// staged in LDS a chunk of candidates at a time with at most P / 1024 + 1 loads per lane per
+// candidate and nothing waiting between them; the J + 1 t-chains of each candidate then run out of
+// LDS (lane per chain, the order and roundings of chain_sum), the ranking, and the kept rows copied
+// with all their loads in flight.
+constexpr int kReuseBlock = 1024;
+constexpr size_t kReuseLds = 156 * 1024;   // the workgroup's LDS: staged cost rows + sums + totals
+
+// per: candidates staged per chunk (launch_reuse sizes it to the LDS)
+__global__ __launch_bounds__(kReuseBlock) void k_reuse(int per, int K, int J, int N, int Kr, int K_gen, int with_extra,
+                                                       const double* src_params, const double* src_state,
+                                                       const double* control, double* params, double* noise,
+                                                       double* state, const double* x_params, const double* x_state,
+                                                       const double* x_control, const double* theta, const int* stop)
 {
     if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
-    __shared__ double part[kReusePart];
     const int n = K + with_extra;
-    double* costs = sh;
-    int* sel = (int*)(sh + n);
-    const int tid = threadIdx.x, bs = blockDim.x;
+    const int tid = threadIdx.x;
+    const int L = J + 1, P = L * N;
     const size_t JN = (size_t)J * N;
-    reuse_totals_block(0, n, K, J, N, src_state, control, x_state, x_control, costs, part);
-    for (int c = tid; c < n; c += bs) {
+    double* stage = sh;                                        // [per][L][N]
+    double* part = sh + (size_t)per * P;                       // [per][L] chain sums
+    double* costs = part + (size_t)per * L;                    // [n]
+    int* sel = (int*)(costs + n);                              // [Kr]
+    for (int c0 = 0; c0 < n; c0 += per) {
+        const int nc = min(per, n - c0);
+        // every load of the chunk in flight (up to 16 candidates per batch), then the LDS stores
+        constexpr int kMaxLoads = 16;
+        for (int i = tid; i < P; i += kReuseBlock) {
+            const bool st = i < N;
+            for (int cb = 0; cb < nc; cb += kMaxLoads) {
+                double v[kMaxLoads];
+#pragma unroll
+                for (int u = 0; u < kMaxLoads; ++u) {
+                    const int c = c0 + min(cb + u, nc - 1);
+                    const double* row = st ? (c < K ? src_state + (size_t)c * N : x_state) + i
+                                           : (c < K ? control + (size_t)c * JN : x_control) + (i - N);
+                    v[u] = *row;
+                }
+#pragma unroll
+                for (int u = 0; u < kMaxLoads; ++u)
+                    if (cb + u < nc) stage[(size_t)(cb + u) * P + i] = v[u];
+            }
+        }
+        __syncthreads();
+        // chain_sum's order: x = v[0], then x += v[t] for t ascending
+        for (int it = tid; it < nc * L; it += kReuseBlock) {
+            const double* v = stage + (size_t)it * N;
+            double x = v[0];
+            for (int t0 = 1; t0 < N; t0 += 16) {
+                double b[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) b[u] = v[min(t0 + u, N - 1)];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (t0 + u < N) x += b[u];
+            }
+            part[it] = x;
+        }
+        __syncthreads();
+        for (int cl = tid; cl < nc; cl += kReuseBlock) {
+            const double* q = part + (size_t)cl * L;
+            double s2 = q[0];
+            for (int d = 0; d < J; ++d) s2 += q[1 + d];
+            costs[c0 + cl] = s2 != s2 ? __builtin_inf() : s2;   // NaN ranks last: the ranks stay a permutation
+        }
+        __syncthreads();   // the stage is reused by the next chunk
+    }
+    for (int c = tid; c < n; c += kReuseBlock) {
         const int ic = c < K ? c : -1;
         const double cc = costs[c];
         int rank = 0;
@@ -183,35 +238,33 @@ __global__ __launch_bounds__(256) void k_reuse(int K, int J, int N, int Kr, int 
     }
     __syncthreads();
     // the kept rows into rows K_gen.. of this iteration's set (the row sets are distinct buffers,
-    // launch_reuse checks it, so the reads need no staging copy)
-    const double* __restrict__ sp = src_params;
-    const double* __restrict__ ss = src_state;
-    // row by row (no per-element 64-bit division), four independent loads in flight per lane
-    const int jn = (int)JN;
-    for (int r = 0; r < Kr; ++r) {
-        const int src = sel[r];
-        const double* prow = src < K ? sp + (size_t)src * JN : x_params;
-        const double* srow = src < K ? ss + (size_t)src * N : x_state;
-        double* pd = params + (size_t)(K_gen + r) * JN;
-        double* nd = noise + (size_t)(K_gen + r) * JN;
-        for (int o0 = tid; o0 < jn; o0 += 4 * bs) {
-            double v[4], th[4];
+    // launch_reuse checks it): params row, noise = params - theta, state row; all loads of a batch
+    // in flight before its stores
+    const int W = (int)JN + N;
+    constexpr int kCopyRows = 16;
+    for (int i = tid; i < W; i += kReuseBlock) {
+        const bool pr = i < (int)JN;
+        const double th = pr ? theta[i] : 0.0;
+        for (int r0 = 0; r0 < Kr; r0 += kCopyRows) {
+            double v[kCopyRows];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int o = min(o0 + u * bs, jn - 1);
-                v[u] = prow[o];
-                th[u] = theta[o];
+            for (int u = 0; u < kCopyRows; ++u) {
+                const int src = sel[min(r0 + u, Kr - 1)];
+                v[u] = pr ? (src < K ? src_params + (size_t)src * JN : x_params)[i]
+                          : (src < K ? src_state + (size_t)src * N : x_state)[i - (int)JN];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int o = o0 + u * bs;
-                if (o < jn) {
-                    pd[o] = v[u];
-                    nd[o] = v[u] - th[u];
+            for (int u = 0; u < kCopyRows; ++u) {
+                const int r = r0 + u;
+                if (r >= Kr) break;
+                if (pr) {
+                    params[(size_t)(K_gen + r) * JN + i] = v[u];
+                    noise[(size_t)(K_gen + r) * JN + i] = v[u] - th;
+                } else {
+                    state[(size_t)(K_gen + r) * N + (i - (int)JN)] = v[u];
                 }
             }
         }
-        for (int t = tid; t < N; t += bs) state[(size_t)(K_gen + r) * N + t] = srow[t];
     }
 }
 
@@ -223,9 +276,13 @@ int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const d
     // k_reuse copies straight from the source rows into rows K_gen..: an in-place call would read
     // rows this same loop already overwrote
     if (src_params == params || src_state == state) return -1;
-    const size_t lds = (size_t)(K + 1) * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
-    if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);   // K in the thousands
-    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(256), lds, s, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
+    const int n = K + with_extra, L = J + 1, P = L * N;
+    const size_t fixed = (size_t)n * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
+    if (fixed + (size_t)(P + L) * sizeof(double) > kReuseLds) return -2;
+    const int per = std::min(n, (int)((kReuseLds - fixed) / ((size_t)(P + L) * sizeof(double))));
+    const size_t lds = (size_t)per * (P + L) * sizeof(double) + fixed;
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);
+    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(kReuseBlock), lds, s, per, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
                        src_control, params, noise, state, x_params, x_state, x_control, theta, stop);
     return 0;
 }

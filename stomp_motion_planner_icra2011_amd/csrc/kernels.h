@@ -343,7 +343,8 @@ void launch_pad_fk(const DevModel& m, const double* start, const double* goal, d
                    hipStream_t s);
 // src_*: the previous iteration's rows (ranked, copied from); params / noise / state: this
 // iteration's rows K_gen.. (written).  The two row sets must be distinct buffers (the copy has no
-// staging pass); returns -1 without launching when they alias.
+// staging pass); returns -1 without launching when they alias, -2 when one candidate's cost rows
+// do not fit the LDS.
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
