@@ -89,18 +89,6 @@ def parse():
     return a
 
 
-def shard_mode(K: int, N: int, reused: int) -> str:
-    """The engine's K-sharded decomposition (engine.cpp, stomp_engine_create): one
-    all-gather of the state-cost rows ("gather") while K N doubles fit 1 MiB and no rows are
-    reused, else three exchanges of block partials ("partials"); STOMP_SHARD_MODE overrides."""
-    if reused > 0 or K > 4096:
-        return "partials"
-    env = os.environ.get("STOMP_SHARD_MODE")
-    if env:
-        return "gather" if env == "gather" else "partials"
-    return "gather" if K * N * 8 <= (1 << 20) else "partials"
-
-
 def workload_name(args) -> str:
     return args.workload + (" (modified)" if args.custom else "")
 
@@ -479,7 +467,7 @@ def main():
             "config": {"workload": f"{workload_name(args)}: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={K} "
                                    f"({K_loc}/GPU), K_r={args.reused}, {args.grid}^3 SDF, S={S} spheres",
                        "global_rollouts": K, "rollouts_per_gpu": K_loc,
-                       "parallelism": f"rollout shard x{world}" + (f" (RCCL, {shard_mode(K, p.N, args.reused)})"
+                       "parallelism": f"rollout shard x{world}" + (f" (RCCL, {e.shard_mode})"
                                                                      if world > 1 else ""),
                        "rollouts_per_s": round(value * K, 1)},
             "roofline": roofline,

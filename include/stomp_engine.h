@@ -258,6 +258,13 @@ int stomp_engine_get_pad_positions(stomp_engine* e, double* out);
 int stomp_engine_set_timing(stomp_engine* e, int32_t enable);
 int stomp_engine_get_timing(stomp_engine* e, const char* name, double* total_ms, int32_t* launches);
 int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count);
+/* The K-sharded decomposition the engine chose: STOMP_SHARD_NONE (one rank),
+ * STOMP_SHARD_PARTIALS (all-reduce + two all-gathers of 64-rollout block partials per iteration) or
+ * STOMP_SHARD_GATHER (one all-gather of the state-cost rows; every rank weights all K). */
+#define STOMP_SHARD_NONE 0
+#define STOMP_SHARD_PARTIALS 1
+#define STOMP_SHARD_GATHER 2
+int stomp_engine_shard_mode(stomp_engine* e, int32_t* mode);
 
 /* Distance-field builder (capped exact EDT, stomp_grid's representation):
  *   value = min(d2, ceil(max_expansion/res)^2)   (the cap must be <= 255 cells)

@@ -1878,6 +1878,13 @@ int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
     return 0;
 }
 
+int stomp_engine_shard_mode(stomp_engine* e, int32_t* mode)
+{
+    if (!e || !mode) return fail(e, STOMP_E_INVALID, "null argument");
+    *mode = e->world == 1 ? STOMP_SHARD_NONE : (e->gather ? STOMP_SHARD_GATHER : STOMP_SHARD_PARTIALS);
+    return 0;
+}
+
 int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, double res, double max_expansion,
                     const double* boxes, int32_t n_boxes, const double* cyl, int32_t n_cyl, uint16_t* out, void* stream)
 {

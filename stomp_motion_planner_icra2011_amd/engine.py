@@ -91,7 +91,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
             "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_pi_reset", "stomp_sdf_build_objects",
             "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
-            "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy"]
+            "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy", "stomp_engine_shard_mode"]
 
 _lib = None
 
@@ -135,6 +135,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_set_timing.argtypes = [P, C.c_int32]
     l.stomp_engine_get_timing.argtypes = [P, C.c_char_p, dp, C.POINTER(C.c_int32)]
     l.stomp_engine_local_rollouts.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    l.stomp_engine_shard_mode.argtypes = [P, C.POINTER(C.c_int32)]
     l.stomp_sdf_build.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double, dp, C.c_int32, dp,
                                   C.c_int32, C.c_void_p, C.c_void_p]
     l.stomp_sdf_build_objects.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double,
@@ -303,6 +304,9 @@ class Engine:
         first, count = C.c_int32(), C.c_int32()
         l.stomp_engine_local_rollouts(self.h, C.byref(first), C.byref(count))
         self.first, self.K_loc = first.value, count.value
+        mode = C.c_int32()
+        _check(l.stomp_engine_shard_mode(self.h, C.byref(mode)))
+        self.shard_mode = {0: "none", 1: "partials", 2: "gather"}[mode.value]
 
     def close(self):
         h = getattr(self, "h", None)

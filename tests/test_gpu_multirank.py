@@ -56,6 +56,7 @@ def test_ranks_iterate_bitwise(world, K, Kr, mode, monkeypatch):
     K_loc = K // world
     for r, e in enumerate(engines):
         assert (e.first, e.K_loc) == (r * K_loc, K_loc)
+        assert e.shard_mode == (mode or "partials")
     o = po.Oracle(p, threads=THREADS)
     iters = range(1, 6)
 
