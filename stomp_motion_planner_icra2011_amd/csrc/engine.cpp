@@ -1264,14 +1264,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         m.phased_lds = 0;
 #endif
         if (getenv("STOMP_DEBUG_PHASED")) fprintf(stderr, "stomp: phased rollout LDS %d B\n", m.phased_lds);
-        {
-            // the wave-local rollout (k_rollout_wave) unless STOMP_ROLLOUT=slot asks for the slot loop
-            const char* rk = getenv("STOMP_ROLLOUT");
-            const size_t lw = rollout_wave_lds(J, N, e->S, m.nseg, m.nops, m.nslots).total;
-            m.wave_block = rollout_wave_block(N);
-            m.wave_lds = (int)lw;
-            if ((rk && std::strcmp(rk, "slot") == 0) || lw + 1024 > kRolloutLdsMax) m.wave_block = 0;
-        }
         if (lds > kRolloutLdsMax)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
                                                     "on one segment), more than %zu", lds, J, N, e->S, m.sph_chunk,

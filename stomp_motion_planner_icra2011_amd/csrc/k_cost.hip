@@ -741,514 +741,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     BLOCK_END();
 }
 
-// ---------------------------------------------------------------- the wave-local rollout
-// One workgroup per rollout with one wave per kWaveOwn free waypoints (BLOCK = 128 for N <= 122,
-// 256 for N <= 244).  After the row prologue, the joint-limit passes and the sin / cos pre-pass
-// (block-wide, as in rollout_body), every wave evaluates its waypoints alone, with no block
-// barrier until the costs: lane l is waypoint t = kWaveOwn w - 1 + l and runs the whole FK program
-// in registers (lanes t < 0 and t >= N run it on start / goal, which is how the padding rows'
-// positions were made: k_pad_fk), looks every sphere up at its own waypoint, takes the velocity
-// taps t - 1, t + 1, t + 2 from its neighbours by lane shuffles, and folds its waypoint's spheres
-// in list order.  Same expressions per (t, s) as rollout_body, so the results are bit-identical.
-constexpr int kWaveR = 8;   // spheres per lookup chunk (one chunk's gathers in flight while the next is issued)
-#ifndef WAVE_VEL_GROUP
-#define WAVE_VEL_GROUP 2
-#endif
-constexpr int kVelGroup = WAVE_VEL_GROUP;   // spheres whose velocities are made together
-static_assert(kWaveR % kVelGroup == 0, "velocity groups tile a chunk");
-
-// wave-uniform table reads through the constant address space (scalar loads); the host pass
-// only parses the device code
-#ifdef __HIP_DEVICE_COMPILE__
-template <class T>
-using cptr = const __attribute__((address_space(4))) T*;
-#else
-template <class T>
-using cptr = const T*;
-#endif
-
-// x of lane l - 1 / l + 1 (DPP wave shifts; lanes 0 / 63 get 0 and are never owned)
-__device__ __forceinline__ double lane_from_prev(double x)
-{
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);          // wave_shr:1
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double lane_from_next(double x)
-{
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);          // wave_shl:1
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-template <int BLOCK>
-__device__ __forceinline__ void rollout_wave_body(const DevModel& m, const CostArgs& a, const int bid)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    __shared__ int flag;
-    const int J = m.J, N = m.N;
-    const RolloutLds L = rollout_wave_lds(J, N, m.S, m.nseg, m.nops, m.nslots);
-    const int nro = a.num_noisy + (a.x_params ? 1 : 0);
-    if (bid >= nro) {
-        // the next iteration's pregen rows (see rollout_body)
-        const NoiseArgs& pa = a.pre_next;
-        double* pA = (double*)(lds_raw + L.nzA);
-        double* pB = (double*)(lds_raw + L.nzB);
-        const int r = bid - nro;
-        if (a.ctl_by_pre && r < a.ctl_rows && !(a.stop && *a.stop)) {
-            pre_row_control<BLOCK>(a.nz, r, pA, pB, threadIdx.x);
-            __syncthreads();
-        }
-        rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
-        if (J <= 8) {
-            pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
-            pregen_meps_ng<BLOCK, 2>(pa, r, pB, threadIdx.x);
-        } else {
-            pregen_eps_ng<BLOCK, 4>(pa, r, pA, pB, threadIdx.x);
-            pregen_meps_ng<BLOCK, 4>(pa, r, pB, threadIdx.x);
-        }
-        return;
-    }
-    __builtin_amdgcn_s_setprio(2);
-    if (a.stop && *a.stop) return;
-    double* traj = (double*)(lds_raw + L.traj);   // J*N
-    double* sinb = (double*)(lds_raw + L.fb);     // [J][N+3]
-    double* cosb = (double*)(lds_raw + L.sv);     // [J][N+3]
-    double* avb = (double*)(lds_raw + L.av);      // [N] costs
-    // the tables (wave-uniform) through the constant address space: scalar loads into SGPRs
-    const unsigned char* ib = (const unsigned char*)m.img;
-    const cptr<DevSphere> sph = (cptr<DevSphere>)(ib + (L.sph - L.sph));
-    const cptr<DevSegment> seg_s = (cptr<DevSegment>)(ib + (L.seg - L.sph));
-    const cptr<FkOp> ops_s = (cptr<FkOp>)(ib + (L.ops - L.sph));
-    const cptr<int> hl_s = (cptr<int>)(ib + (L.hl - L.sph));
-    const cptr<double> jlim_s = (cptr<double>)(ib + (L.jlim - L.sph));
-
-    STAMP(0);
-    BLOCK_BEGIN();
-    const int e = bid, tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    constexpr int NW = BLOCK / 64;
-    const bool extra = e == a.num_noisy;
-    const int member = extra ? a.x_member : a.member;
-    double* zA = (double*)(lds_raw + L.nzA);
-    double* zB = (double*)(lds_raw + L.nzB);
-    const bool gen = a.fused_noise == 1 && !extra;
-    const bool pre = a.fused_noise == 2 && !extra;
-    PreChunk pc0;
-    const bool priced = a.ctl_by_pre;
-    const int pr = e + a.row0;
-    if (pre) {
-        if (priced) pre_chunk_load<BLOCK, false>(a.nz, pr, 0, tid, pc0);
-        else pre_chunk_load<BLOCK>(a.nz, pr, 0, tid, pc0);
-    }
-    if (gen) {
-        rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
-    } else if (!pre) {
-        const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
-        const bool xc = extra && a.x_ctl;
-        for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
-            double v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = prm[min(idx0 + tid + u * BLOCK, J * N - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int idx = idx0 + tid + u * BLOCK;
-                if (idx < J * N) {
-                    traj[idx] = v[u];
-                    if (xc) {
-                        a.x_prm[idx] = v[u];
-                        a.x_nse[idx] = 0.0;
-                        const int d = idx / N, i = idx - d * N;
-                        zA[d * m.Nall + i + 6] = v[u] + 0.0;
-                    }
-                }
-            }
-        }
-        if (xc) rollout_control<BLOCK>(a.nz, 0, zA, zB, tid, a.x_ctl);
-    }
-    if (gen) {
-        rollout_project<BLOCK>(a.nz, e, traj, zA, zB, tid);
-    } else if (pre) {
-        if (priced) rollout_from_pre<BLOCK, true, false>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
-        else rollout_from_pre<BLOCK>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
-    }
-    if (tid == 0) flag = 0;
-    __syncthreads();
-    STAMP(1);
-
-    // ---- handleJointLimits (stomp_optimizer.cpp:562-616): the limited joints dealt round-robin
-    // over the waves; a wave runs the passes of up to kJlGroup of its joints in lockstep on
-    // register-resident rows (lane l: waypoints l, l + 64, ...), so their Q^-1 column loads are in
-    // flight together.  Same argmax (first index on ties), amounts and updates as rollout_body.
-    {
-        constexpr int kJlGroup = 4;
-        auto jl_argmax = [&](const double* v, double jmin, double jmax) -> int {
-            double cand = 0.0;
-            int ci = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = lane + 64 * u;
-                if (t < N) {
-                    const double x = v[u];
-                    double absamt = 0.0;
-                    if (x > jmax) absamt = fabs(jmax - x);
-                    else if (x < jmin) absamt = fabs(jmin - x);
-                    if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }
-                }
-            }
-            const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
-            const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
-            const unsigned mh = wave_max_u32(hi);
-            const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
-            if ((mh | ml) == 0u) return -1;
-            const bool match = hi == mh && lo == ml;
-            int cm = 0;
-            for (int blk = 0; blk * 64 < N; ++blk) {
-                const unsigned long long b = __ballot(match && (ci >> 6) == blk);
-                if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
-            }
-            return cm;
-        };
-        auto jl_run = [&](const int* js, int g) {
-            double v[kJlGroup][4], lo[kJlGroup], hi[kJlGroup];
-            bool live[kJlGroup];
-#pragma unroll
-            for (int q = 0; q < kJlGroup; ++q) {
-                const int j = js[q];   // js[q >= g] repeats js[0]
-                lo[q] = jlim_s[2 * j];
-                hi[q] = jlim_s[2 * j + 1];
-                live[q] = q < g;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[q][u] = traj[j * N + min(lane + 64 * u, N - 1)];
-            }
-            for (int pass = 0; pass < 11; ++pass) {
-                int c[kJlGroup];
-                bool any = false;
-#pragma unroll
-                for (int q = 0; q < kJlGroup; ++q) {
-                    c[q] = -1;
-                    if (live[q]) {
-                        c[q] = jl_argmax(v[q], lo[q], hi[q]);
-                        live[q] = c[q] >= 0;
-                        any |= live[q];
-                    }
-                }
-                if (!any) break;
-                // every group member's column and diagonal in flight (unconditional, clamped)
-                double qv[kJlGroup][4], qd[kJlGroup];
-#pragma unroll
-                for (int q = 0; q < kJlGroup; ++q) {
-                    const int j = js[q];   // js[q >= g] repeats js[0]
-                    const double* Q = m.QT + ((size_t)j * N + (size_t)max(c[q], 0)) * N;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) qv[q][u] = Q[min(lane + 64 * u, N - 1)];
-                    qd[q] = Q[max(c[q], 0)];
-                }
-#pragma unroll
-                for (int q = 0; q < kJlGroup; ++q) {
-                    if (!live[q]) continue;
-                    const int cm = c[q];
-                    double vu = v[q][0];
-#pragma unroll
-                    for (int u = 1; u < 4; ++u)
-                        if ((cm >> 6) == u) vu = v[q][u];
-                    const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
-                    const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
-                    const unsigned vhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), cm & 63);
-                    const double x = __longlong_as_double((long long)(((unsigned long long)vhi << 32) | vlo));
-                    const double amount = x > hi[q] ? hi[q] - x : lo[q] - x;
-                    const double mult = amount / qd[q];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (lane + 64 * u < N) v[q][u] += mult * qv[q][u];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < kJlGroup; ++q) {
-                if (q >= g) break;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int t = lane + 64 * u;
-                    if (t < N) traj[js[q] * N + t] = v[q][u];
-                }
-            }
-        };
-        __builtin_amdgcn_s_setprio(3);
-        unsigned mine = 0;   // this wave's joints (wave-uniform)
-        for (int j = 0, k = 0; j < J; ++j)
-            if (hl_s[j] && k++ % NW == wv) mine |= 1u << j;
-        while (mine) {
-            int js[kJlGroup], g = 0;
-#pragma unroll
-            for (int q = 0; q < kJlGroup; ++q) {
-                js[q] = mine ? __builtin_ctz(mine) : js[0];
-                if (mine) { mine &= mine - 1; g = q + 1; }
-            }
-            jl_run(js, g);
-        }
-        __builtin_amdgcn_s_setprio(2);
-        __syncthreads();
-    }
-    STAMP(2);
-    double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
-    if (tout)
-        for (int idx = tid; idx < J * N; idx += BLOCK) tout[idx] = traj[idx];
-    // (sin, cos) of every joint angle at waypoints -1 .. N + 1 (start, the limited trajectory,
-    // goal), three independent chains per lane
-    {
-        const int N3 = N + 3, JN3 = J * N3;
-        for (int i0 = tid; i0 - tid < JN3; i0 += 3 * BLOCK) {
-            double q[3], sn[3], cs[3];
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-                const int idx = min(i0 + u * BLOCK, JN3 - 1);
-                const int d = idx / N3, c = idx - d * N3;
-                q[u] = c == 0 ? m.start[d] : (c > N ? m.goal[d] : traj[d * N + c - 1]);
-            }
-#pragma unroll
-            for (int u = 0; u < 3; ++u) det_sincos(q[u], &sn[u], &cs[u]);
-            // unconditional stores (a lane past the end rewrites the last element with its own
-            // value), so the three chains are not sunk into separate branches
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-                const int idx = min(i0 + u * BLOCK, JN3 - 1);
-                sinb[idx] = sn[u];
-                cosb[idx] = cs[u];
-            }
-        }
-    }
-    __syncthreads();
-    STAMP(3);
-
-    // ---- the wave's waypoints: FK program, lookups, velocities and the fold
-    const int W = (N + kWaveOwn - 1) / kWaveOwn;
-    const int t = kWaveOwn * wv - 1 + lane;
-    const bool own = wv < W && lane >= 1 && lane <= kWaveOwn && t < N;
-    double cum = 0.0, state = 0.0;
-    bool col = false;
-    if (wv < W) {
-        __builtin_amdgcn_s_setprio(3);
-        const int N3 = N + 3;
-        const int ti = min(max(t + 1, 0), N + 2);
-        const double* sn = sinb + ti;
-        const double* cs = cosb + ti;
-        Frame C, S0, S1;
-        auto fk_step = [&](const FkOp& o) {
-            if (o.seg < 0) return;
-            const DevSegment sg = seg_s[o.seg];
-            double st = 0.0, ct = 1.0;
-            if (sg.q_index >= 0) {
-                st = sn[sg.q_index * N3];
-                ct = cs[sg.q_index * N3];
-            }
-            fk_op(sg, o.base, o.save, st, ct, C, S0, S1);
-        };
-        const int nops = m.nops;
-        auto fk_advance = [&](int op) -> int {
-            for (; op < nops; ++op) {
-                const FkOp o = ops_s[op];
-                fk_step(o);
-                if (o.sph_end > o.sph_begin) return op;
-            }
-            return nops;
-        };
-        // a chunk: up to kWaveR consecutive spheres of one segment, the frame they hang on and
-        // their voxels' d2
-        struct Chunk {
-            Frame F;
-            unsigned d[kWaveR];
-            unsigned ok;   // bit u: voxel u inside the grid
-            int b, n;      // first sphere, spheres (uniform)
-        };
-        // sphere position at this lane's waypoint (stomp_collision_point.h:138-141)
-        auto place = [&](const Frame& F, const double* pos, double* x) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-                x[i] = F.R[3 * i] * pos[0] + F.R[3 * i + 1] * pos[1] + F.R[3 * i + 2] * pos[2] + F.p[i];
-        };
-        // the chunk's lookups, every gather in flight.  Branch-free (one basic block, so the
-        // lookups interleave): slots past n repeat the chunk's last sphere and are ignored, and an
-        // out-of-grid lane loads cell 0 and discards it.
-        auto issue = [&](Chunk& ch, int op, int b) {
-            const int n = min(kWaveR, ops_s[op].sph_end - b);
-            ch.b = b;
-            ch.n = n;
-            ch.F = C;
-            unsigned okm = 0;
-#pragma unroll
-            for (int u = 0; u < kWaveR; ++u) {
-                double pos[3], x[3];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) pos[i] = sph[b + min(u, n - 1)].pos[i];
-                place(C, pos, x);
-                bool ok;
-                const unsigned idx = sdf_cell(m, x, ok);
-                ch.d[u] = m.sdf[idx];
-                okm |= (unsigned)ok << u;
-            }
-            ch.ok = okm;
-        };
-        // potentials, velocities of the non-zero pairs and the fold, in sphere order.  The
-        // velocities go kVelGroup spheres at a time (one uniform branch per group that holds a
-        // non-zero pair in this wave), so their latency chains overlap.
-        auto process = [&](const Chunk& ch) {
-            const int n = ch.n, b = ch.b;
-            double av[kWaveR];
-            unsigned nzm = 0;
-#pragma unroll
-            for (int u = 0; u < kWaveR; ++u) {
-                const int sq = b + min(u, n - 1);
-                const int zl = sph[sq].zero_lim, cl = sph[sq].col_lim;
-                const bool in = own & (u < n);
-                const int d2 = (ch.ok >> u) & 1u ? (int)ch.d[u] : 0;
-                col |= in & (d2 < cl);
-                nzm |= (unsigned)(in & (d2 < zl)) << u;
-                av[u] = 0.0;
-            }
-#pragma unroll
-            for (int g0 = 0; g0 < kWaveR; g0 += kVelGroup) {
-                if (!__ballot((nzm >> g0) & ((1u << kVelGroup) - 1u))) continue;   // uniform
-                // positions (tap t), then the taps t - 1, t + 1, t + 2 from the neighbouring lanes
-                double y[kVelGroup][7][3];
-#pragma unroll
-                for (int v = 0; v < kVelGroup; ++v) {
-                    double pos[3];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) pos[i] = sph[b + min(g0 + v, n - 1)].pos[i];
-                    place(ch.F, pos, y[v][3]);
-                }
-#pragma unroll
-                for (int v = 0; v < kVelGroup; ++v)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        y[v][2][c] = lane_from_prev(y[v][3][c]);
-                        y[v][4][c] = lane_from_next(y[v][3][c]);
-                    }
-#pragma unroll
-                for (int v = 0; v < kVelGroup; ++v)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) y[v][5][c] = lane_from_next(y[v][4][c]);
-#pragma unroll
-                for (int v = 0; v < kVelGroup; ++v) {
-                    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-#pragma unroll
-                    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
-                        const double c = m.vel_coef[kk];
-                        if (c == 0.0) continue;
-                        v0 += c * y[v][kk][0];
-                        v1 += c * y[v][kk][1];
-                        v2 += c * y[v][kk][2];
-                    }
-                    const double spd = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                    const int sq = b + min(g0 + v, n - 1);
-                    DevSphere sp;
-                    sp.radius = sph[sq].radius;
-                    sp.clearance = sph[sq].clearance;
-                    sp.inv_clearance = sph[sq].inv_clearance;
-                    const int d2 = (ch.ok >> (g0 + v)) & 1u ? (int)ch.d[g0 + v] : 0;
-                    const double pot = potential(sp, sdf_metres(m, (unsigned)d2));
-                    av[g0 + v] = (nzm >> (g0 + v)) & 1u ? pot * spd : 0.0;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kWaveR; ++u) {
-                const double c2 = cum + av[u];
-                const double s2 = state + c2;
-                const bool live = u < n;   // uniform
-                cum = live ? c2 : cum;
-                state = live ? s2 : state;
-            }
-        };
-        auto next = [&](int& op, int& b) {
-            if (b + kWaveR < ops_s[op].sph_end) {
-                b += kWaveR;
-            } else {
-                op = fk_advance(op + 1);
-                if (op < nops) b = ops_s[op].sph_begin;
-            }
-        };
-        int op = fk_advance(0);
-        int b = op < nops ? ops_s[op].sph_begin : 0;
-        STAMP(7);
-        int ci = 0;   // chunk count (stamp index only)
-#ifdef WAVE_PIPELINE
-        Chunk A, B;
-        if (op < nops) issue(A, op, b);
-        // two register sets in turn: chunk k + 1's FK and gathers are issued before chunk k is used
-        while (op < nops) {
-            int op2 = op, b2 = b;
-            next(op2, b2);
-            if (op2 < nops) issue(B, op2, b2);
-            STAMP(20 + 2 * ci);
-            process(A);
-            STAMP(21 + 2 * ci);
-            ++ci;
-            op = op2; b = b2;
-            if (op >= nops) break;
-            next(op2, b2);
-            if (op2 < nops) issue(A, op2, b2);
-            STAMP(20 + 2 * ci);
-            process(B);
-            STAMP(21 + 2 * ci);
-            ++ci;
-            op = op2; b = b2;
-        }
-#else
-        while (op < nops) {
-            Chunk A;
-            issue(A, op, b);
-            STAMP(20 + 2 * ci);
-            process(A);
-            STAMP(21 + 2 * ci);
-            ++ci;
-            next(op, b);
-        }
-#endif
-        __builtin_amdgcn_s_setprio(2);
-    }
-    STAMP(4);
-    if (col) flag = 1;
-    double cost = 0.0;
-    if (own) {
-        cost = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
-        avb[t] = cost;
-    }
-    __syncthreads();
-    if (own) {
-        double* so = extra ? a.x_state : a.state_out + (long long)e * N;
-        so[t] = cost;
-    }
-    if (tid == 0) {
-        const bool cf = !flag && !(member == 0 && m.pad_collision);
-        uint8_t* cfo = extra ? a.x_cf : (a.cf_out ? a.cf_out + e : nullptr);
-        double* to = extra ? a.x_total : (a.total_out ? a.total_out + e : nullptr);
-        if (cfo) *cfo = cf ? 1 : 0;
-        if (to) {
-            double s = 0.0;   // costs.sum() (:1155), sequential
-            int k = 0;
-            for (; k + 8 <= N; k += 8) {
-                double v[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = avb[k + q];
-#pragma unroll
-                for (int q = 0; q < 8; ++q) s += v[q];
-            }
-            for (; k < N; ++k) s += avb[k];
-            *to = s;
-        }
-    }
-    STAMP(5);
-    BLOCK_END();
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, 2) void k_rollout_wave(DevModel m, CostArgs a)
-{
-    rollout_wave_body<BLOCK>(m, a, blockIdx.x);
-}
-
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
@@ -1374,28 +866,11 @@ int rollout_blocks_per_cu(size_t lds_total)
     return by_regs < by_lds ? by_regs : by_lds;
 }
 
-int rollout_wave_block(int N)
-{
-    const int w = (N + kWaveOwn - 1) / kWaveOwn;
-    return w <= 2 ? 128 : (w <= 4 ? 256 : 0);
-}
-
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int nro = a.num_noisy + (a.x_params ? 1 : 0);
     const int blocks = nro + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
-    if (m.wave_block > 0) {
-        const size_t lw = m.wave_lds;
-        if (m.wave_block == 128) {
-            if (lw > 64 * 1024) lds_opt_in((const void*)k_rollout_wave<128>, lw);
-            hipLaunchKernelGGL((k_rollout_wave<128>), dim3(blocks), dim3(128), lw, s, m, a);
-        } else {
-            if (lw > 64 * 1024) lds_opt_in((const void*)k_rollout_wave<256>, lw);
-            hipLaunchKernelGGL((k_rollout_wave<256>), dim3(blocks), dim3(256), lw, s, m, a);
-        }
-        return;
-    }
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
     if (kWideBlock != kBlock && nro <= m.cus && m.phased_lds > 0) {
         const size_t lp = m.phased_lds;

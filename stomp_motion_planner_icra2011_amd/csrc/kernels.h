@@ -74,9 +74,6 @@ struct DevModel {
                                 // launch's rollouts fit one per CU)
     int phased_lds;             // dynamic LDS of the phased wide rollout (every slot's frame and every
                                 // sphere's a value resident), 0 when it does not fit a CU
-    int wave_block;             // the wave-local rollout (k_rollout_wave): threads per workgroup (64 per
-                                // kWaveOwn waypoints), 0 when the shape does not fit it
-    int wave_lds;               // its dynamic LDS
     const unsigned long long* img;   // the rollout kernel's LDS table image (RolloutLds from .sph on)
     int img_words;              // 8-byte words of it copied to LDS (up to .pad, or .total with pad_lds)
     const DevSegment* segs;
@@ -141,39 +138,6 @@ __host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_s
     l.jlim = align16(l.hl + (size_t)J * sizeof(int));
     l.pad = align16(l.jlim + (size_t)2 * J * sizeof(double));
     l.total = l.pad + (pad_lds ? (size_t)36 * S * sizeof(double) : 0);
-    return l;
-}
-
-// The wave-local rollout (k_rollout_wave): wave w of a rollout's workgroup evaluates free
-// waypoints [kWaveOwn w, kWaveOwn (w + 1)) on lanes 1 .. kWaveOwn, lane l being waypoint
-// kWaveOwn w - 1 + l, so the velocity taps t - 1 .. t + 2 of every owned waypoint are in the wave.
-constexpr int kWaveOwn = 61;
-// traj [J][N]; sines and cosines of every joint angle at waypoints -1 .. N + 1 ([J][N + 3]: start,
-// the joint-limited trajectory, goal), aliased by the noise phase's two buffers (dead by then);
-// the costs [N]; then the table image as in rollout_lds (its relative offsets are the same)
-__host__ __device__ inline RolloutLds rollout_wave_lds(int J, int N, int S, int nseg, int nops, int nslots)
-{
-    RolloutLds l{};
-    l.traj = 0;
-    const size_t jn3 = (size_t)J * (N + 3);
-    l.fb = l.traj + (size_t)J * N * sizeof(double);
-    l.sv = l.fb + jn3 * sizeof(double);
-    const size_t nzw = (size_t)(N + kBandBatch) * noise_jp(J) > (size_t)J * (N + 12)
-                           ? (size_t)(N + kBandBatch) * noise_jp(J) : (size_t)J * (N + 12);
-    l.nzA = l.fb;
-    l.nzB = l.nzA + nzw * sizeof(double);
-    size_t end = l.sv + jn3 * sizeof(double);
-    if (l.nzB + nzw * sizeof(double) > end) end = l.nzB + nzw * sizeof(double);
-    l.av = end;
-    l.nzl = l.av + (size_t)N * sizeof(double);
-    l.sph = align16(l.nzl);
-    l.seg = align16(l.sph + (size_t)S * sizeof(DevSphere));
-    l.ops = align16(l.seg + (size_t)nseg * sizeof(DevSegment));
-    l.slot = align16(l.ops + (size_t)nops * sizeof(FkOp));
-    l.hl = align16(l.slot + (size_t)(nslots + 1) * sizeof(int));
-    l.jlim = align16(l.hl + (size_t)J * sizeof(int));
-    l.pad = align16(l.jlim + (size_t)2 * J * sizeof(double));
-    l.total = l.pad;
     return l;
 }
 
@@ -345,8 +309,6 @@ bool cost_supported(const DevModel& m);
 size_t rollout_lds_bytes(const DevModel& m, int pad_lds);   // dynamic LDS of the rollout kernel
 size_t rollout_phased_lds_bytes(const DevModel& m);        // of the phased wide rollout, 0: does not fit
 size_t rollout_static_lds();                                 // its static LDS
-// threads per workgroup of the wave-local rollout for N free waypoints (0: N too large for it)
-int rollout_wave_block(int N);
 int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS and register limits)
 // LDS per CU is 160 KiB (MI355X_MICROARCH.md), but three 49.5 KB rollout workgroups did not
 // co-reside on one CU in our residency measurements (tools/stamps.py) while three 46.9 KB

@@ -48,15 +48,7 @@ def show(name, block, labels):
         prev = v[i]
 
 
-WAVE = os.environ.get("STOMP_ROLLOUT", "wave") != "slot"
-
-
 def cost_label(i):
-    if WAVE:
-        if 20 <= i < 60:
-            return f"chunk {(i - 20) // 2}: " + ["next FK + issue", "process"][(i - 20) % 2]
-        return {0: "start", 1: "row + tables", 2: "joint limits", 3: "traj out + sincos", 7: "first FK + issue",
-                4: "main loop done", 5: "end"}.get(i, str(i))
     if i in (61, 62, 63):
         return {61: "control terms (thread 0)", 62: "control terms barrier", 63: "control costs stored (t0)"}[i]
     if 100 <= i < 140:
