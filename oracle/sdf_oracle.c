@@ -124,55 +124,316 @@ static double dotcol(const double* v, const double* B, int k)
     return v[0] * B[k] + v[1] * B[3 + k] + v[2] * B[6 + k];
 }
 
-/* supporting planes of the convex hull of V: every vertex triple i < j < k in order spans a
- * candidate plane n = (vj - vi) x (vk - vi) / |.|, d = -(n . vi); it is kept (flipped so that
- * the hull lies on the negative side) when no vertex lies more than eps on each side of it,
- * unless a kept plane already has the same normal (n . n' > 1 - 1e-12) and offset (within eps).
- * eps = 1e-9 (1 + max |coordinate|).  Deterministic: the engine runs the same loops. */
+/* Supporting planes of the convex hull of V (bodies::ConvexMesh's qhull hull, restated).
+ *   1. Vertices with identical coordinates are merged (the first index kept): COLLADA meshes
+ *      repeat positions.
+ *   2. Incremental hull of the unique vertices in index order: a first tetrahedron (vertex 0, the
+ *      one farthest from it, the one farthest from their line, the one farthest from their
+ *      plane), then each vertex that lies more than eps outside some face replaces the faces it
+ *      sees by a fan over their horizon (directed edges found through a hash of (a, b) -> face).
+ *   3. Faces whose planes agree (n . n' > 1 - 1e-12, |d - d'| <= eps) form one facet; a facet's
+ *      plane is spanned by the first triple i < j < k of its vertices (index order) that is not
+ *      collinear (|u x w| > 1e-12 |u| |w|) and leaves every hull vertex within eps on one side,
+ *      n = (vj - vi) x (vk - vi) / |.|, d = -(n . vi), flipped so the hull lies on the negative
+ *      side.  Facets are emitted in the order of their triples, a plane equal to one already
+ *      emitted (same normal and offset test) skipped.
+ * eps = 1e-9 (1 + max |coordinate|).  O(V log V + V F) instead of the O(V^4) triple scan.  The
+ * engine (csrc/engine.cpp hull_planes) implements the same steps in C++. */
+typedef struct {
+    int v[3];
+    double n[3], d;
+    int alive;
+} hull_face;
+
+typedef struct {
+    unsigned long long* key;
+    int* val;
+    size_t cap, used;
+} edge_map;
+
+static size_t em_slot(const edge_map* m, unsigned long long k)
+{
+    size_t h = (size_t)((k * 0x9E3779B97F4A7C15ull) >> 17) & (m->cap - 1);
+    while (m->val[h] >= 0 && m->key[h] != k) h = (h + 1) & (m->cap - 1);
+    return h;
+}
+
+static int em_grow(edge_map* m)
+{
+    edge_map n = {0};
+    n.cap = m->cap ? 2 * m->cap : 1024;
+    n.key = (unsigned long long*)malloc(sizeof(unsigned long long) * n.cap);
+    n.val = (int*)malloc(sizeof(int) * n.cap);
+    if (!n.key || !n.val) { free(n.key); free(n.val); return -1; }
+    for (size_t i = 0; i < n.cap; ++i) n.val[i] = -1;
+    for (size_t i = 0; i < m->cap; ++i)
+        if (m->val[i] >= 0) {
+            const size_t h = em_slot(&n, m->key[i]);
+            n.key[h] = m->key[i];
+            n.val[h] = m->val[i];
+            ++n.used;
+        }
+    free(m->key); free(m->val);
+    *m = n;
+    return 0;
+}
+
+static int em_put(edge_map* m, int a, int b, int f)
+{
+    if (2 * (m->used + 1) > m->cap && em_grow(m)) return -1;
+    const unsigned long long k = ((unsigned long long)(unsigned)a << 32) | (unsigned)b;
+    const size_t h = em_slot(m, k);
+    if (m->val[h] < 0) ++m->used;
+    m->key[h] = k;
+    m->val[h] = f;
+    return 0;
+}
+
+static int em_get(const edge_map* m, int a, int b)
+{
+    const unsigned long long k = ((unsigned long long)(unsigned)a << 32) | (unsigned)b;
+    return m->val[em_slot(m, k)];
+}
+
+static const double* hv(const double* V, int i) { return V + 3 * (size_t)i; }
+
+/* plane through vertices a, b, c: unit normal of (b - a) x (c - a) and offset; 0 when collinear */
+static int plane3(const double* V, int a, int b, int c, double* n, double* d)
+{
+    const double* A = hv(V, a); const double* B = hv(V, b); const double* C = hv(V, c);
+    const double u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+    const double w[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+    n[0] = u[1] * w[2] - u[2] * w[1]; n[1] = u[2] * w[0] - u[0] * w[2]; n[2] = u[0] * w[1] - u[1] * w[0];
+    const double len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const double lu = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]), lw = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (!(len > 1e-12 * lu * lw) || !(len > 0.0)) return 0;
+    n[0] /= len; n[1] /= len; n[2] /= len;
+    *d = -(n[0] * A[0] + n[1] * A[1] + n[2] * A[2]);
+    return 1;
+}
+
+static double sdist(const double* n, double d, const double* p) { return n[0] * p[0] + n[1] * p[1] + n[2] * p[2] + d; }
+
+static const double* g_sort_v;
+static int cmp_xyz(const void* a, const void* b)
+{
+    const int i = *(const int*)a, j = *(const int*)b;
+    for (int k = 0; k < 3; ++k) {
+        const double x = g_sort_v[3 * (size_t)i + k], y = g_sort_v[3 * (size_t)j + k];
+        if (x < y) return -1;
+        if (x > y) return 1;
+    }
+    return i < j ? -1 : (i > j);
+}
+
+static int cmp_int(const void* a, const void* b)
+{
+    const int i = *(const int*)a, j = *(const int*)b;
+    return i < j ? -1 : (i > j);
+}
+
+typedef struct { int t[3]; double n[3], d; } hull_facet;
+
+static int cmp_facet(const void* a, const void* b)
+{
+    const hull_facet* x = (const hull_facet*)a; const hull_facet* y = (const hull_facet*)b;
+    for (int k = 0; k < 3; ++k)
+        if (x->t[k] != y->t[k]) return x->t[k] < y->t[k] ? -1 : 1;
+    return 0;
+}
+
 int so_hull_planes(const double* V, int nv, double* planes, int max_planes)
 {
+    if (nv < 4) return -1;
     double ext = 0.0;
     for (int i = 0; i < 3 * nv; ++i)
         if (fabs(V[i]) > ext) ext = fabs(V[i]);
     const double eps = 1e-9 * (1.0 + ext);
-    int np = 0;
-    for (int i = 0; i < nv; ++i)
-        for (int j = i + 1; j < nv; ++j)
-            for (int k = j + 1; k < nv; ++k) {
-                const double* a = V + 3 * i;
-                const double* b = V + 3 * j;
-                const double* c = V + 3 * k;
-                const double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-                const double w[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-                double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
-                const double len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-                if (!(len > eps * eps)) continue;   /* (nearly) collinear */
-                n[0] /= len; n[1] /= len; n[2] /= len;
-                double d = -(n[0] * a[0] + n[1] * a[1] + n[2] * a[2]);
-                double smax = -1e300, smin = 1e300;
-                for (int q = 0; q < nv; ++q) {
-                    const double sd = n[0] * V[3 * q] + n[1] * V[3 * q + 1] + n[2] * V[3 * q + 2] + d;
-                    if (sd > smax) smax = sd;
-                    if (sd < smin) smin = sd;
-                }
-                if (smax <= eps) {
-                    /* hull below the plane */
-                } else if (smin >= -eps) {
-                    n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; d = -d;
-                } else {
-                    continue;
-                }
-                int dup = 0;
-                for (int p = 0; p < np && !dup; ++p) {
-                    const double* e = planes + 4 * p;
-                    dup = n[0] * e[0] + n[1] * e[1] + n[2] * e[2] > 1.0 - 1e-12 && fabs(d - e[3]) <= eps;
-                }
-                if (dup) continue;
-                if (np == max_planes) return -1;
-                planes[4 * np] = n[0]; planes[4 * np + 1] = n[1]; planes[4 * np + 2] = n[2]; planes[4 * np + 3] = d;
-                ++np;
+    int rc = -1, nu = 0, nf = 0, capf = 0, nh = 0;
+    int* ord = (int*)malloc(sizeof(int) * (size_t)nv);
+    int* uq = (int*)malloc(sizeof(int) * (size_t)nv);
+    unsigned char* onhull = (unsigned char*)calloc((size_t)nv, 1);
+    int* hullv = (int*)malloc(sizeof(int) * (size_t)nv);
+    hull_face* F = NULL;
+    hull_facet* fc = NULL;
+    int *vis = NULL, *hor = NULL, *grp = NULL, *fv = NULL;
+    edge_map em = {0};
+    if (!ord || !uq || !onhull || !hullv) goto done;
+    /* 1. unique vertices */
+    for (int i = 0; i < nv; ++i) ord[i] = i;
+    g_sort_v = V;
+    qsort(ord, (size_t)nv, sizeof(int), cmp_xyz);
+    for (int i = 0; i < nv; ++i) {
+        const double* p = hv(V, ord[i]);
+        if (i > 0) {
+            const double* q = hv(V, ord[i - 1]);
+            if (p[0] == q[0] && p[1] == q[1] && p[2] == q[2]) continue;   /* the group's first index came first */
+        }
+        uq[nu++] = ord[i];
+    }
+    qsort(uq, (size_t)nu, sizeof(int), cmp_int);
+    if (nu < 4) goto done;
+    /* 2. the first tetrahedron */
+    {
+        const int a = uq[0];
+        int b = -1, c = -1, e = -1;
+        double best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double* p = hv(V, uq[i]); const double* A = hv(V, a);
+            const double dx = p[0] - A[0], dy = p[1] - A[1], dz = p[2] - A[2];
+            const double r = sqrt(dx * dx + dy * dy + dz * dz);
+            if (r > best) { best = r; b = uq[i]; }
+        }
+        if (b < 0) goto done;
+        best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double* A = hv(V, a); const double* B = hv(V, b); const double* p = hv(V, uq[i]);
+            const double u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+            const double w[3] = {p[0] - A[0], p[1] - A[1], p[2] - A[2]};
+            const double x[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+            const double r = sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) / sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+            if (r > best) { best = r; c = uq[i]; }
+        }
+        if (c < 0) goto done;
+        double n[3], d;
+        if (!plane3(V, a, b, c, n, &d)) goto done;
+        best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double r = fabs(sdist(n, d, hv(V, uq[i])));
+            if (r > best) { best = r; e = uq[i]; }
+        }
+        if (e < 0) goto done;
+        const int tet[4][3] = {{a, b, c}, {a, e, b}, {b, e, c}, {c, e, a}};
+        double ctr[3];
+        for (int k = 0; k < 3; ++k) ctr[k] = (hv(V, a)[k] + hv(V, b)[k] + hv(V, c)[k] + hv(V, e)[k]) / 4.0;
+        capf = 64;
+        F = (hull_face*)malloc(sizeof(hull_face) * (size_t)capf);
+        if (!F) goto done;
+        for (int f = 0; f < 4; ++f) {
+            hull_face* h = &F[nf++];
+            h->v[0] = tet[f][0]; h->v[1] = tet[f][1]; h->v[2] = tet[f][2];
+            if (!plane3(V, h->v[0], h->v[1], h->v[2], h->n, &h->d)) goto done;
+            if (sdist(h->n, h->d, ctr) > 0.0) {   /* orient outward */
+                const int t = h->v[1]; h->v[1] = h->v[2]; h->v[2] = t;
+                if (!plane3(V, h->v[0], h->v[1], h->v[2], h->n, &h->d)) goto done;
             }
-    return np >= 4 ? np : -1;
+            h->alive = 1;
+            for (int k = 0; k < 3; ++k)
+                if (em_put(&em, h->v[k], h->v[(k + 1) % 3], f)) goto done;
+        }
+        onhull[a] = onhull[b] = onhull[c] = onhull[e] = 1;
+    }
+    /* the rest, in index order */
+    vis = (int*)malloc(sizeof(int) * 16);
+    hor = (int*)malloc(sizeof(int) * 32);
+    int capv = 16, caph = 16;
+    if (!vis || !hor) goto done;
+    for (int i = 1; i < nu; ++i) {
+        const int p = uq[i];
+        if (onhull[p]) continue;
+        const double* P = hv(V, p);
+        int nvis = 0;
+        for (int f = 0; f < nf; ++f) {
+            if (!F[f].alive || !(sdist(F[f].n, F[f].d, P) > eps)) continue;
+            if (nvis == capv) { capv *= 2; int* t = (int*)realloc(vis, sizeof(int) * (size_t)capv); if (!t) goto done; vis = t; }
+            vis[nvis++] = f;
+        }
+        if (!nvis) continue;   /* inside, or within eps of the hull */
+        for (int q = 0; q < nvis; ++q) F[vis[q]].alive = 2;   /* visible */
+        int nhor = 0;
+        for (int q = 0; q < nvis; ++q) {
+            const hull_face* h = &F[vis[q]];
+            for (int k = 0; k < 3; ++k) {
+                const int ea = h->v[k], eb = h->v[(k + 1) % 3];
+                const int o = em_get(&em, eb, ea);
+                if (o >= 0 && F[o].alive == 2) continue;   /* interior edge of the visible region */
+                if (nhor == caph) { caph *= 2; int* t = (int*)realloc(hor, sizeof(int) * 2 * (size_t)caph); if (!t) goto done; hor = t; }
+                hor[2 * nhor] = ea; hor[2 * nhor + 1] = eb; ++nhor;
+            }
+        }
+        for (int q = 0; q < nvis; ++q) F[vis[q]].alive = 0;
+        for (int q = 0; q < nhor; ++q) {
+            if (nf == capf) { capf *= 2; hull_face* t = (hull_face*)realloc(F, sizeof(hull_face) * (size_t)capf); if (!t) goto done; F = t; }
+            hull_face* h = &F[nf];
+            h->v[0] = hor[2 * q]; h->v[1] = hor[2 * q + 1]; h->v[2] = p;
+            h->alive = 1;
+            if (!plane3(V, h->v[0], h->v[1], h->v[2], h->n, &h->d)) { h->n[0] = h->n[1] = h->n[2] = 0.0; h->d = 0.0; }
+            for (int k = 0; k < 3; ++k)
+                if (em_put(&em, h->v[k], h->v[(k + 1) % 3], nf)) goto done;
+            ++nf;
+        }
+        onhull[p] = 1;
+    }
+    /* 3. facets: faces grouped by plane, each facet's plane from its first spanning triple */
+    for (int f = 0; f < nf; ++f)
+        if (F[f].alive)
+            for (int k = 0; k < 3; ++k) onhull[F[f].v[k]] = 2;
+    for (int i = 0; i < nu; ++i)
+        if (onhull[uq[i]] == 2) hullv[nh++] = uq[i];
+    grp = (int*)malloc(sizeof(int) * (size_t)nf);
+    fv = (int*)malloc(sizeof(int) * 3 * (size_t)nf);
+    fc = (hull_facet*)malloc(sizeof(hull_facet) * (size_t)nf);
+    if (!grp || !fv || !fc) goto done;
+    for (int f = 0; f < nf; ++f) grp[f] = -1;
+    int nfc = 0;
+    for (int f = 0; f < nf; ++f) {
+        if (!F[f].alive || grp[f] >= 0) continue;
+        int m = 0;
+        for (int g = f; g < nf; ++g) {
+            if (!F[g].alive || grp[g] >= 0) continue;
+            if (g != f && !(F[f].n[0] * F[g].n[0] + F[f].n[1] * F[g].n[1] + F[f].n[2] * F[g].n[2] > 1.0 - 1e-12 &&
+                            fabs(F[f].d - F[g].d) <= eps))
+                continue;
+            grp[g] = f;
+            for (int k = 0; k < 3; ++k) fv[m++] = F[g].v[k];
+        }
+        qsort(fv, (size_t)m, sizeof(int), cmp_int);
+        int mu = 0;
+        for (int q = 0; q < m; ++q)
+            if (!mu || fv[mu - 1] != fv[q]) fv[mu++] = fv[q];
+        int found = 0;
+        for (int x = 0; x < mu && !found; ++x)
+            for (int y = x + 1; y < mu && !found; ++y)
+                for (int z = y + 1; z < mu && !found; ++z) {
+                    double n[3], d;
+                    if (!plane3(V, fv[x], fv[y], fv[z], n, &d)) continue;
+                    double smax = -1e300, smin = 1e300;
+                    for (int q = 0; q < nh; ++q) {
+                        const double sd = sdist(n, d, hv(V, hullv[q]));
+                        if (sd > smax) smax = sd;
+                        if (sd < smin) smin = sd;
+                    }
+                    if (smax <= eps) {
+                    } else if (smin >= -eps) {
+                        n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; d = -d;
+                    } else {
+                        continue;
+                    }
+                    hull_facet* o = &fc[nfc++];
+                    o->t[0] = fv[x]; o->t[1] = fv[y]; o->t[2] = fv[z];
+                    o->n[0] = n[0]; o->n[1] = n[1]; o->n[2] = n[2]; o->d = d;
+                    found = 1;
+                }
+    }
+    qsort(fc, (size_t)nfc, sizeof(hull_facet), cmp_facet);
+    int np = 0;
+    for (int q = 0; q < nfc; ++q) {
+        int dup = 0;
+        for (int p2 = 0; p2 < np && !dup; ++p2) {
+            const double* e = planes + 4 * p2;
+            dup = fc[q].n[0] * e[0] + fc[q].n[1] * e[1] + fc[q].n[2] * e[2] > 1.0 - 1e-12 && fabs(fc[q].d - e[3]) <= eps;
+        }
+        if (dup) continue;
+        if (np == max_planes) goto done;
+        planes[4 * np] = fc[q].n[0]; planes[4 * np + 1] = fc[q].n[1]; planes[4 * np + 2] = fc[q].n[2];
+        planes[4 * np + 3] = fc[q].d;
+        ++np;
+    }
+    rc = np >= 4 ? np : -1;
+done:
+    free(ord); free(uq); free(onhull); free(hullv); free(F); free(fc); free(vis); free(hor); free(grp); free(fv);
+    free(em.key); free(em.val);
+    return rc;
 }
 
 /* the mesh body: centre of the vertices' bounding box and the largest distance of a vertex from

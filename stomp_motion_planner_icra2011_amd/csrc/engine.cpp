@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kernels.h"
@@ -1968,58 +1969,225 @@ int stomp_sdf_build(int32_t nx, int32_t ny, int32_t nz, const double* origin, do
 }
 
 // bodies::ConvexMesh's convex hull (third party: qhull in geometric_shapes) as its supporting
-// planes, appended to `planes` as (n, d) with unit outward n and n.x + d = 0 on the face: every
-// vertex triple i < j < k in order spans a candidate plane, kept (flipped so the hull lies on the
-// negative side) when no vertex lies more than eps on each side of it, unless a kept plane has
-// the same normal and offset.  eps = 1e-9 (1 + max |coordinate|).  Returns the number of planes
-// (-1: no volume).  oracle/sdf_oracle.c so_hull_planes runs the same loops.
+// planes, appended to `planes` as (n, d) with unit outward n and n.x + d = 0 on the face; the steps
+// of oracle/sdf_oracle.c so_hull_planes, restated in C++ (same expressions, so the same planes):
+// merge vertices with identical coordinates (first index kept), incremental hull of the unique
+// vertices in index order (first tetrahedron, then each vertex more than eps outside a face
+// replaces the faces it sees by a fan over their horizon), faces with the same plane (n . n' >
+// 1 - 1e-12, |d - d'| <= eps) merged into facets, each facet's plane spanned by the first
+// non-collinear triple of its vertices (|u x w| > 1e-12 |u| |w|) that leaves every hull vertex
+// within eps on one side, facets in the order of those triples.  eps = 1e-9 (1 + max |coordinate|).
+// O(V log V + V F).  Returns the number of planes (-1: no volume).
+namespace hull {
+struct Face {
+    int v[3];
+    double n[3], d;
+    int alive;
+};
+inline const double* at(const double* V, int i) { return V + 3 * (size_t)i; }
+inline bool plane3(const double* V, int a, int b, int c, double* n, double* d)
+{
+    const double* A = at(V, a);
+    const double* B = at(V, b);
+    const double* C = at(V, c);
+    const double u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+    const double w[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+    n[0] = u[1] * w[2] - u[2] * w[1];
+    n[1] = u[2] * w[0] - u[0] * w[2];
+    n[2] = u[0] * w[1] - u[1] * w[0];
+    const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const double lu = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    const double lw = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    if (!(len > 1e-12 * lu * lw) || !(len > 0.0)) return false;
+    n[0] /= len;
+    n[1] /= len;
+    n[2] /= len;
+    *d = -(n[0] * A[0] + n[1] * A[1] + n[2] * A[2]);
+    return true;
+}
+inline double sdist(const double* n, double d, const double* p) { return n[0] * p[0] + n[1] * p[1] + n[2] * p[2] + d; }
+inline uint64_t edge_key(int a, int b) { return ((uint64_t)(unsigned)a << 32) | (unsigned)b; }
+}  // namespace hull
+
 static int hull_planes(const double* V, int nv, std::vector<double>& planes)
 {
+    using namespace hull;
+    if (nv < 4) return -1;
     double ext = 0.0;
     for (int i = 0; i < 3 * nv; ++i)
         if (std::fabs(V[i]) > ext) ext = std::fabs(V[i]);
     const double eps = 1e-9 * (1.0 + ext);
+    // unique vertices
+    std::vector<int> ord(nv), uq;
+    for (int i = 0; i < nv; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int i, int j) {
+        for (int k = 0; k < 3; ++k) {
+            const double x = V[3 * (size_t)i + k], y = V[3 * (size_t)j + k];
+            if (x != y) return x < y;
+        }
+        return i < j;
+    });
+    for (int i = 0; i < nv; ++i) {
+        const double* p = at(V, ord[i]);
+        if (i > 0) {
+            const double* q = at(V, ord[i - 1]);
+            if (p[0] == q[0] && p[1] == q[1] && p[2] == q[2]) continue;
+        }
+        uq.push_back(ord[i]);
+    }
+    std::sort(uq.begin(), uq.end());
+    const int nu = (int)uq.size();
+    if (nu < 4) return -1;
+    std::vector<unsigned char> onhull(nv, 0);
+    std::vector<Face> F;
+    std::unordered_map<uint64_t, int> em;
+    {
+        const int a = uq[0];
+        int b = -1, c = -1, e = -1;
+        double best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double* p = at(V, uq[i]);
+            const double* A = at(V, a);
+            const double dx = p[0] - A[0], dy = p[1] - A[1], dz = p[2] - A[2];
+            const double r = std::sqrt(dx * dx + dy * dy + dz * dz);
+            if (r > best) { best = r; b = uq[i]; }
+        }
+        if (b < 0) return -1;
+        best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double* A = at(V, a);
+            const double* B = at(V, b);
+            const double* p = at(V, uq[i]);
+            const double u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+            const double w[3] = {p[0] - A[0], p[1] - A[1], p[2] - A[2]};
+            const double x[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+            const double r = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]) / std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+            if (r > best) { best = r; c = uq[i]; }
+        }
+        if (c < 0) return -1;
+        double n[3], d;
+        if (!plane3(V, a, b, c, n, &d)) return -1;
+        best = eps;
+        for (int i = 1; i < nu; ++i) {
+            const double r = std::fabs(sdist(n, d, at(V, uq[i])));
+            if (r > best) { best = r; e = uq[i]; }
+        }
+        if (e < 0) return -1;
+        const int tet[4][3] = {{a, b, c}, {a, e, b}, {b, e, c}, {c, e, a}};
+        double ctr[3];
+        for (int k = 0; k < 3; ++k) ctr[k] = (at(V, a)[k] + at(V, b)[k] + at(V, c)[k] + at(V, e)[k]) / 4.0;
+        for (int f = 0; f < 4; ++f) {
+            Face h;
+            h.v[0] = tet[f][0]; h.v[1] = tet[f][1]; h.v[2] = tet[f][2];
+            if (!plane3(V, h.v[0], h.v[1], h.v[2], h.n, &h.d)) return -1;
+            if (sdist(h.n, h.d, ctr) > 0.0) {
+                std::swap(h.v[1], h.v[2]);
+                if (!plane3(V, h.v[0], h.v[1], h.v[2], h.n, &h.d)) return -1;
+            }
+            h.alive = 1;
+            F.push_back(h);
+            for (int k = 0; k < 3; ++k) em[edge_key(h.v[k], h.v[(k + 1) % 3])] = f;
+        }
+        onhull[a] = onhull[b] = onhull[c] = onhull[e] = 1;
+    }
+    std::vector<int> vis, hor;
+    for (int i = 1; i < nu; ++i) {
+        const int p = uq[i];
+        if (onhull[p]) continue;
+        const double* P = at(V, p);
+        vis.clear();
+        for (int f = 0; f < (int)F.size(); ++f)
+            if (F[f].alive && sdist(F[f].n, F[f].d, P) > eps) vis.push_back(f);
+        if (vis.empty()) continue;
+        for (int f : vis) F[f].alive = 2;
+        hor.clear();
+        for (int f : vis)
+            for (int k = 0; k < 3; ++k) {
+                const int ea = F[f].v[k], eb = F[f].v[(k + 1) % 3];
+                const auto it = em.find(edge_key(eb, ea));
+                if (it != em.end() && F[it->second].alive == 2) continue;
+                hor.push_back(ea);
+                hor.push_back(eb);
+            }
+        for (int f : vis) F[f].alive = 0;
+        for (size_t q = 0; q < hor.size(); q += 2) {
+            Face h;
+            h.v[0] = hor[q]; h.v[1] = hor[q + 1]; h.v[2] = p;
+            h.alive = 1;
+            if (!plane3(V, h.v[0], h.v[1], h.v[2], h.n, &h.d)) { h.n[0] = h.n[1] = h.n[2] = 0.0; h.d = 0.0; }
+            const int id = (int)F.size();
+            F.push_back(h);
+            for (int k = 0; k < 3; ++k) em[edge_key(h.v[k], h.v[(k + 1) % 3])] = id;
+        }
+        onhull[p] = 1;
+    }
+    // facets
+    for (const Face& f : F)
+        if (f.alive)
+            for (int k = 0; k < 3; ++k) onhull[f.v[k]] = 2;
+    std::vector<int> hullv;
+    for (int i = 0; i < nu; ++i)
+        if (onhull[uq[i]] == 2) hullv.push_back(uq[i]);
+    struct Facet {
+        int t[3];
+        double n[3], d;
+    };
+    std::vector<Facet> fc;
+    std::vector<int> grp(F.size(), -1), fv;
+    const int nf = (int)F.size();
+    for (int f = 0; f < nf; ++f) {
+        if (!F[f].alive || grp[f] >= 0) continue;
+        fv.clear();
+        for (int g = f; g < nf; ++g) {
+            if (!F[g].alive || grp[g] >= 0) continue;
+            if (g != f && !(F[f].n[0] * F[g].n[0] + F[f].n[1] * F[g].n[1] + F[f].n[2] * F[g].n[2] > 1.0 - 1e-12 &&
+                            std::fabs(F[f].d - F[g].d) <= eps))
+                continue;
+            grp[g] = f;
+            for (int k = 0; k < 3; ++k) fv.push_back(F[g].v[k]);
+        }
+        std::sort(fv.begin(), fv.end());
+        fv.erase(std::unique(fv.begin(), fv.end()), fv.end());
+        const int mu = (int)fv.size();
+        bool found = false;
+        for (int x = 0; x < mu && !found; ++x)
+            for (int y = x + 1; y < mu && !found; ++y)
+                for (int z = y + 1; z < mu && !found; ++z) {
+                    double n[3], d;
+                    if (!plane3(V, fv[x], fv[y], fv[z], n, &d)) continue;
+                    double smax = -1e300, smin = 1e300;
+                    for (int q : hullv) {
+                        const double sd = sdist(n, d, at(V, q));
+                        if (sd > smax) smax = sd;
+                        if (sd < smin) smin = sd;
+                    }
+                    if (smax <= eps) {
+                    } else if (smin >= -eps) {
+                        n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; d = -d;
+                    } else {
+                        continue;
+                    }
+                    fc.push_back(Facet{{fv[x], fv[y], fv[z]}, {n[0], n[1], n[2]}, d});
+                    found = true;
+                }
+    }
+    std::sort(fc.begin(), fc.end(), [](const Facet& a, const Facet& b) {
+        for (int k = 0; k < 3; ++k)
+            if (a.t[k] != b.t[k]) return a.t[k] < b.t[k];
+        return false;
+    });
     const size_t first = planes.size();
     int np = 0;
-    for (int i = 0; i < nv; ++i)
-        for (int j = i + 1; j < nv; ++j)
-            for (int k = j + 1; k < nv; ++k) {
-                const double* a = V + 3 * i;
-                const double* b = V + 3 * j;
-                const double* c = V + 3 * k;
-                const double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-                const double w[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-                double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
-                const double len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-                if (!(len > eps * eps)) continue;
-                n[0] /= len;
-                n[1] /= len;
-                n[2] /= len;
-                double d = -(n[0] * a[0] + n[1] * a[1] + n[2] * a[2]);
-                double smax = -1e300, smin = 1e300;
-                for (int q = 0; q < nv; ++q) {
-                    const double sd = n[0] * V[3 * q] + n[1] * V[3 * q + 1] + n[2] * V[3 * q + 2] + d;
-                    if (sd > smax) smax = sd;
-                    if (sd < smin) smin = sd;
-                }
-                if (smax <= eps) {
-                } else if (smin >= -eps) {
-                    n[0] = -n[0];
-                    n[1] = -n[1];
-                    n[2] = -n[2];
-                    d = -d;
-                } else {
-                    continue;
-                }
-                bool dup = false;
-                for (int p = 0; p < np && !dup; ++p) {
-                    const double* e = planes.data() + first + 4 * p;
-                    dup = n[0] * e[0] + n[1] * e[1] + n[2] * e[2] > 1.0 - 1e-12 && std::fabs(d - e[3]) <= eps;
-                }
-                if (dup) continue;
-                planes.insert(planes.end(), {n[0], n[1], n[2], d});
-                ++np;
-            }
+    for (const Facet& q : fc) {
+        bool dup = false;
+        for (int p2 = 0; p2 < np && !dup; ++p2) {
+            const double* e = planes.data() + first + 4 * p2;
+            dup = q.n[0] * e[0] + q.n[1] * e[1] + q.n[2] * e[2] > 1.0 - 1e-12 && std::fabs(q.d - e[3]) <= eps;
+        }
+        if (dup) continue;
+        planes.insert(planes.end(), {q.n[0], q.n[1], q.n[2], q.d});
+        ++np;
+    }
     if (np < 4) {
         planes.resize(first);
         return -1;

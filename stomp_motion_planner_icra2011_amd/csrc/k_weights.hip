@@ -353,11 +353,6 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
             return;
         }
         __syncthreads();
-        if (tid < TCW) {
-            double ps = 0.0;
-            for (int b = 0; b < nb; ++b) ps += part[b * TCW + tid];
-            ps_s[tid] = ps;
-        }
     } else {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) v[k] = colok ? a.prob[(size_t)min(rs + RS * k, K - 1) * JN + cl] : 0.0;
@@ -367,19 +362,30 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
                 for (int b = 0; b < a.nb_total; ++b) ps += a.psum_all[(size_t)b * JN + c];
             ps_s[tid] = ps;
         }
+        __syncthreads();
     }
-    __syncthreads();
     STAMP(3);
     {
-        const double ps = ps_s[cc];
+        // every lane sums its column's block partials itself (the same sequence on every lane of
+        // the column: no extra barrier), then all EPT divisions at once (branch-free, so their
+        // chains overlap) before the predicated stores
+        double ps;
+        if (a.mode == W_USUM) {
+            ps = ps_s[cc];
+        } else {
+            ps = 0.0;
+            for (int b = 0; b < nb; ++b) ps += part[b * TCW + cc];
+        }
+        double pn[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) pn[k] = v[k] / ps;
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const int r = rs + RS * k;
-            if (r >= K) continue;
-            if (!colok) { V[vidx(r, cc, TCW)] = 0.0; continue; }
-            const double pn = v[k] / ps;
-            a.prob[(size_t)r * JN + c] = pn;
-            V[vidx(r, cc, TCW)] = nz[k] * pn;
+            if (r < K) {
+                V[vidx(r, cc, TCW)] = colok ? nz[k] * pn[k] : 0.0;
+                if (colok) a.prob[(size_t)r * JN + c] = pn[k];
+            }
         }
     }
     __syncthreads();

@@ -309,3 +309,37 @@ def test_mesh_rejects_flat_vertices():
                           np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0]], np.float64))
     with pytest.raises(ValueError):
         po.sdf_build_objects(grid, [flat])
+
+
+def test_hull_planes_large_meshes_fast_and_exact():
+    # the hull was O(V^4) (every vertex triple against every vertex); a link mesh of
+    # thousands of (repeated COLLADA) vertices now takes milliseconds and still agrees with qhull
+    import time
+    from scipy.spatial import ConvexHull
+    rng = np.random.default_rng(11)
+    s = rng.normal(size=(2500, 3))
+    s /= np.linalg.norm(s, axis=1)[:, None]
+    v = np.concatenate([s, s[::3]])   # repeated positions, as COLLADA meshes have
+    t0 = time.time()
+    ours = po.hull_planes(v)
+    assert time.time() - t0 < 5.0
+    h = ConvexHull(v)
+    P = rng.uniform(-1.05, 1.05, (20000, 3))
+    a = np.all(P @ ours[:, :3].T + ours[:, 3] <= 0, axis=1)
+    b = np.all(P @ h.equations[:, :3].T + h.equations[:, 3] <= 0, axis=1)
+    assert np.array_equal(a, b)
+
+
+def test_hull_planes_subdivided_faces_and_edges():
+    # a cube whose faces and edges carry extra (coplanar / collinear) vertices: exactly its six
+    # planes, each normal exact (no plane from a nearly collinear triple along an edge)
+    g = np.linspace(-0.5, 0.5, 9)
+    pts = []
+    for x in g:
+        for y in g:
+            for z in (-0.5, 0.5):
+                pts += [(x, y, z), (x, z, y), (z, x, y)]
+    ours = po.hull_planes(np.array(pts))
+    assert len(ours) == 6
+    for p in ours:
+        assert np.isclose(np.abs(p[:3]).max(), 1.0, atol=1e-15) and np.isclose(p[3], -0.5, atol=1e-15)
