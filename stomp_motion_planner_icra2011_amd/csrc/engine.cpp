@@ -60,6 +60,10 @@ struct LocalGroup {
     std::vector<char> joined;
     long long phase = 0;    // completed barrier phases
     int arrived = 0;
+    // the decomposition every rank must run (gather, K, J, N), set by the first rank to join: a
+    // rank that disagrees would post different collectives, so its creation fails instead
+    bool has_sig = false;
+    long long sig[4] = {0, 0, 0, 0};
     bool broken = false;    // a rank timed out: every later barrier fails at once
     // all ranks arrive (or the wait times out: a rank not driven from a thread of its own)
     bool barrier(std::unique_lock<std::mutex>& lk)
@@ -967,6 +971,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         // the rollout launch and no reuse.
         const bool can = e->pre_on && e->pre_host == 1 && e->Kr == 0 && e->K <= kSumBlock * 64;
         const char* sm = std::getenv("STOMP_SHARD_MODE");
+        if (world > 1 && sm && std::strcmp(sm, "gather") == 0 && !can) {
+            // not honoured silently: a rank falling back to partials would post other collectives
+            rc = fail(e, STOMP_E_UNSUPPORTED, "STOMP_SHARD_MODE=gather needs the pregen rows in the rollout launch "
+                                              "and no reused rollouts (K_r = %d, J = %d)", e->Kr, e->J);
+            g_last_error = e->err; release(e); delete e; return rc;
+        }
         // STOMP_DEBUG_GATHER_RANKS=W: a one-device engine times rank 0 of W gather-mode ranks (its
         // K / W rollouts, all K rows made and weighted; nothing exchanged, so results are not the
         // sharded ones: a timing hook)
@@ -1347,6 +1357,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             if (g->world != world) CREATE_TRY(fail(e, STOMP_E_COMM, "local group of %d ranks, engine world_size %d",
                                                    g->world, world));
             if (g->joined[e->rank]) CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d joined the local group twice", e->rank));
+            const long long sig[4] = {e->gather ? 1 : 0, e->K, J, N};
+            if (g->has_sig && std::memcmp(sig, g->sig, sizeof sig) != 0)
+                CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d: decomposition (%s, K=%lld, J=%d, N=%d) differs from the group's "
+                                "(%s, K=%lld, J=%lld, N=%lld)", e->rank, e->gather ? "gather" : "partials", (long long)e->K,
+                                J, N, g->sig[0] ? "gather" : "partials", g->sig[1], g->sig[2], g->sig[3]));
+            std::memcpy(g->sig, sig, sizeof sig);
+            g->has_sig = true;
             g->joined[e->rank] = 1;
             g->slot[e->rank].device = e->device;
             for (int q = 0; q < world; ++q)   // copies between the ranks' devices go peer to peer
@@ -1373,6 +1390,23 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         std::memcpy(&id, d->comm_id, sizeof id);
         if (ncclCommInitRank(&e->comm, world, id, e->rank) != ncclSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "ncclCommInitRank failed"));
+        // every rank must run the same decomposition and shape, or the per-iteration collectives
+        // would not pair up (one all-gather against an all-reduce and two all-gathers): one
+        // all-reduce(max) of (x, -x) pairs at creation
+        const double h[8] = {e->gather ? 1.0 : 0.0, e->gather ? -1.0 : 0.0, (double)e->K, -(double)e->K,
+                             (double)J,           -(double)J,            (double)N,    -(double)N};
+        double* d_sig = nullptr;
+        CREATE_TRY(dev_alloc(e, &d_sig, 8));
+        double r[8];
+        if (hipMemcpyAsync(d_sig, h, sizeof h, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+            ncclAllReduce(d_sig, d_sig, 8, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess ||
+            hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            CREATE_TRY(fail(e, STOMP_E_COMM, "decomposition check across ranks failed"));
+        for (int k = 0; k < 8; k += 2)
+            if (r[k] != -r[k + 1])
+                CREATE_TRY(fail(e, STOMP_E_COMM, "ranks disagree on the K-sharded decomposition (gather, K, J, N; "
+                                "entry %d: max %g, min %g)", k / 2, r[k], -r[k + 1]));
     } else if (e->split_modes && world == 1) {
         // STOMP_DEBUG_RCCL_ONE_RANK=1 (with the sharded-modes hook): a one-rank communicator,
         // so the sharded path's RCCL all-reduce / all-gathers run on a one-GPU box

@@ -256,7 +256,14 @@ class Engine:
         if sdf_device_ptr is not None:
             grid_ptr, on_dev = sdf_device_ptr, 1
         else:
-            self._sdf = np.ascontiguousarray(p.sdf, np.uint16)
+            # ABI v4: the field is the integer squared cell distance (PropagationDistanceField's
+            # distance_square_), not metres; a float field would truncate to "in collision" silently
+            sdf = np.asarray(p.sdf)
+            if not np.issubdtype(sdf.dtype, np.integer):
+                raise TypeError(f"problem.sdf must hold integer squared cell distances (uint16), got {sdf.dtype}")
+            if sdf.size and (int(sdf.min()) < 0 or int(sdf.max()) > 65535):
+                raise ValueError("problem.sdf squared cell distances must lie in [0, 65535]")
+            self._sdf = np.ascontiguousarray(sdf, np.uint16)
             grid_ptr, on_dev = self._sdf.ctypes.data, 0
         d.grid = stomp_grid(g.n, g.n, g.n, (C.c_double * 3)(*g.origin), g.resolution, C.c_void_p(grid_ptr), on_dev)
         d.discretization = pr.trajectory_discretization

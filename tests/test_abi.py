@@ -7,6 +7,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from stomp_motion_planner_icra2011_amd import engine as eng
@@ -116,3 +117,15 @@ def test_multi_rank_arguments_checked(rank, comm, msg):
 def test_local_group_ids_are_distinct():
     a, b = eng.comm_local_id(2), eng.comm_local_id(2)
     assert a[:8] == b"STOMPLOC" and b[:8] == b"STOMPLOC" and a != b and len(a) == 128
+
+
+def test_float_field_rejected():
+    # ABI v4 holds the field as integer squared cell distances: a field in metres is refused, not
+    # truncated to "everything in collision" 
+    p = pb.make_problem(grid_n=16, num_rollouts=10, num_reused_rollouts=0)
+    p.sdf = np.full((16, 16, 16), 0.35, np.float32)
+    with pytest.raises(TypeError, match="integer squared cell distances"):
+        eng.Engine(p)
+    p.sdf = np.full((16, 16, 16), 70000, np.int64)
+    with pytest.raises(ValueError, match="65535"):
+        eng.Engine(p)

@@ -166,3 +166,23 @@ def test_ranks_with_state_terms_bitwise(mode, monkeypatch):
             np.testing.assert_array_equal(pp, pr[64 * r:64 * (r + 1)])
     for e in engines:
         e.close()
+
+
+def test_gather_request_not_honoured_fails(monkeypatch):
+    # STOMP_SHARD_MODE=gather with reused rollouts cannot run gather mode: creation fails instead of
+    # silently falling back to partials (a rank on the other mode would post other collectives)
+    p = pb.make_problem(grid_n=32, num_rollouts=128, num_reused_rollouts=64)
+    monkeypatch.setenv("STOMP_SHARD_MODE", "gather")
+    with pytest.raises(RuntimeError, match="STOMP_SHARD_MODE=gather"):
+        eng.Engine(p, rank=0, world_size=2, comm_id=eng.comm_local_id(2))
+
+
+def test_ranks_disagreeing_on_the_decomposition_fail(monkeypatch):
+    p = pb.make_problem(grid_n=32, num_rollouts=128, num_reused_rollouts=0)
+    gid = eng.comm_local_id(2)
+    monkeypatch.setenv("STOMP_SHARD_MODE", "gather")
+    e0 = eng.Engine(p, rank=0, world_size=2, comm_id=gid)
+    monkeypatch.setenv("STOMP_SHARD_MODE", "partials")
+    with pytest.raises(RuntimeError, match="differs from the group"):
+        eng.Engine(p, rank=1, world_size=2, comm_id=gid)
+    del e0
