@@ -23,6 +23,19 @@ namespace stomp {
 __device__ __forceinline__ double lds_seq_sum(const double* p, int stride, int count)
 {
     double s = 0.0;
+    if (count == kSumBlock) {
+        // a whole block: no per-term predicate, so the chain is the adds alone (a select after
+        // every add made it three dependent operations per term)
+#pragma unroll
+        for (int q0 = 0; q0 < kSumBlock; q0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = p[(q0 + q) * stride];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s += v[q];
+        }
+        return s;
+    }
     for (int q0 = 0; q0 < count; q0 += 16) {
         double v[16];
 #pragma unroll
@@ -373,19 +386,28 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
         if (a.mode == W_USUM) {
             ps = ps_s[cc];
         } else {
-            ps = 0.0;
-            for (int b = 0; b < nb; ++b) ps += part[b * TCW + cc];
+            ps = lds_seq_sum(part + cc, TCW, nb);   // b ascending from 0.0, the loads batched
         }
-        double pn[EPT];
+        double pn[EPT], w[EPT];
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) pn[k] = v[k] / ps;
+        for (int k = 0; k < EPT; ++k) {
+            pn[k] = v[k] / ps;
+            w[k] = colok ? nz[k] * pn[k] : 0.0;
+        }
+        // every quotient made here, before any predicated store (otherwise the divisions are sunk
+        // into the stores' branches one by one, and each store's data register is waited on
+        // before the next branch reuses it)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) asm volatile("" ::"v"(pn[k]), "v"(w[k]));
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const int r = rs + RS * k;
-            if (r < K) {
-                V[vidx(r, cc, TCW)] = colok ? nz[k] * pn[k] : 0.0;
-                if (colok) a.prob[(size_t)r * JN + c] = pn[k];
-            }
+            if (r < K) V[vidx(r, cc, TCW)] = w[k];
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int r = rs + RS * k;
+            if (r < K && colok) a.prob[(size_t)r * JN + c] = pn[k];
         }
     }
     __syncthreads();
@@ -399,11 +421,7 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
     if (a.mode == W_USUM) return;
     __syncthreads();
     STAMP(4);
-    if (tid < TCW && colok) {
-        double u = 0.0;
-        for (int b = 0; b < nb; ++b) u += part[b * TCW + tid];
-        a.u[c] = u;
-    }
+    if (tid < TCW && colok) a.u[c] = lds_seq_sum(part + tid, TCW, nb);
     STAMP(5);
 }
 
