@@ -148,11 +148,10 @@ struct stomp_engine {
     double *d_mm = nullptr, *d_psum_part = nullptr, *d_psum_all = nullptr, *d_u_part = nullptr, *d_u_all = nullptr;
     int K_gen = 0;
     // pregen (K_r = 0, fused noise phase): the normals, eps = sigma L z and M eps of iteration
-    // it + 1 are made by extra low-priority blocks of iteration it's rollout launch (pre_host 1;
-    // or of its weights launch, pre_host 2); the rollout launch of it + 1 reads them.  Two
-    // buffers, by iteration parity: a rollout launch reads one and fills the other.
+    // it + 1 are made by extra low-priority blocks of iteration it's rollout launch; the rollout
+    // launch of it + 1 reads them.  Two buffers, by iteration parity: a rollout launch reads one
+    // and fills the other.
     bool pre_on = false;
-    int pre_host = 1;
     int pre_it = -1;                  // iteration whose rows are in d_pre_eps / d_pre_meps[it & 1] (enqueued)
     double *d_pre_eps[2] = {nullptr, nullptr}, *d_pre_meps[2] = {nullptr, nullptr};
     // the last iteration left its rows in d_pre_eps (rows_eps) instead of copying them into
@@ -687,11 +686,7 @@ int begin_generate(stomp_engine* e)
 int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
 {
     const int member = it - 1;
-#ifndef STOMP_SEPARATE_NOISE
     const bool fused = e->J <= 16;   // rollout_project: at most four 4-joint column groups
-#else
-    const bool fused = false;
-#endif
     // With fused noise the reuse step runs after the rollout launch: the generated rows go to
     // the other row set, and the launch also evaluates the pending noiseless rollout that the
     // ranking needs (so K_r > 0 iterations pipeline like K_r = 0 ones).  Otherwise k_noise
@@ -712,7 +707,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     if (fused) na.row_begin = e->gather ? e->rows : num_gen;
     // every local row generated (K_r = 0): eps and M eps come from k_pregen
     const bool pre = fused && e->pre_on && num_gen == e->K_loc;
-    if (e->gather && !(pre && e->pre_host == 1)) return fail(e, STOMP_E_INVALID, "gather mode needs the pregen rows");
+    if (e->gather && !pre) return fail(e, STOMP_E_INVALID, "gather mode needs the pregen rows");
     // outside the optimize loop the rows stay in the pregen buffer: the weights read eps there
     // and nothing else needs the noise / params rows on the device (reuse is off with pregen).
     // The optimize loop keeps the copies: after its stop the pregen blocks of the iterations
@@ -739,7 +734,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         ca.nz = na;
         ca.params = e->d_params; ca.stride = (long long)e->J * e->N; ca.num_noisy = num_gen;
         ca.member = member; ca.state_out = e->d_state;
-        if (pre && e->pre_host == 1) {
+        if (pre) {
             ca.pre_rows = e->rows;
             ca.pre_next = pregen_args(e, it + 1);
             ca.ctl_by_pre = 1;
@@ -787,27 +782,19 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     wa.tc = weights_tile(e->rows);
     wa.nb_total = e->K / kSumBlock;
     wa.mm = e->d_mm; wa.psum_part = e->d_psum_part; wa.psum_all = e->d_psum_all; wa.u_part = e->d_u_part;
-    // the first weights launch carries the next iteration's pregen rows
-    NoiseArgs next{};
-    const NoiseArgs* carry = nullptr;
-    if (pre && e->pre_host == 2) {
-        next = pregen_args(e, it + 1);
-        carry = &next;
-        e->pre_it = it + 1;
-    }
     {
         Timed tm(e, T_WEIGHTS);
         if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
         if (!e->split_modes) {
             wa.mode = W_FUSED;
-            launch_weights(wa, e->stream, carry);
+            launch_weights(wa, e->stream);
         } else {
             // the sharded decomposition; with one rank (debug hook) the all-reduce is the
             // identity and the all-gathers are device copies
             const size_t JN = (size_t)e->J * e->N;
             const size_t nb_loc = (size_t)e->K_loc / kSumBlock;
             wa.mode = W_MINMAX;
-            launch_weights(wa, e->stream, carry);
+            launch_weights(wa, e->stream);
             int rc = exchange_max(e, e->d_mm, 2 * JN);
             if (rc) return rc;
             wa.mode = W_PSUM;
@@ -952,16 +939,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         rc = fail(e, STOMP_E_INVALID, "at most %d rollouts per device", kSumBlock * 64);
         g_last_error = e->err; release(e); delete e; return rc;
     }
-    {
-        // STOMP_PREGEN=0: the rollout kernel draws its own noise (A/B hook)
-        const char* pg = std::getenv("STOMP_PREGEN");
-#ifndef STOMP_SEPARATE_NOISE
-        const char* ph = std::getenv("STOMP_PREGEN_HOST");
-        e->pre_host = (ph && std::strcmp(ph, "weights") == 0) ? 2 : 1;
-        e->pre_on = e->Kr == 0 && e->J <= 16 && (e->pre_host == 1 || weights_carry_pregen(e->K_loc)) &&
-                    !(pg && pg[0] == '0');
-#endif
-    }
+    e->pre_on = e->Kr == 0 && e->J <= 16;   // the fused noise phase (rollout_project) takes J <= 16
     {
         // the K-sharded decomposition.  gather: one all-gather of the state-cost rows
         // per iteration, every rank making and pricing all K noise rows; partials: three exchanges
@@ -969,7 +947,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         // the state rows of all K rollouts are at most 1 MiB (cfg2: 396 KB; cfg3's 6.5 MB stay
         // partials), STOMP_SHARD_MODE=gather|partials to choose.  Gather needs the pregen rows in
         // the rollout launch and no reuse.
-        const bool can = e->pre_on && e->pre_host == 1 && e->Kr == 0 && e->K <= kSumBlock * 64;
+        const bool can = e->pre_on && e->Kr == 0 && e->K <= kSumBlock * 64;
         const char* sm = std::getenv("STOMP_SHARD_MODE");
         if (world > 1 && sm && std::strcmp(sm, "gather") == 0 && !can) {
             // not honoured silently: a rank falling back to partials would post other collectives
@@ -1255,9 +1233,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             if (o.save >= 0 && first_save == (int)e->ops.size()) first_save = i;
         }
         m.sincos_pre = m.nsaves >= 1 && J <= 12 * m.nsaves && first_save > last_joint ? 1 : 0;
-#ifdef NO_SINCOS_PRE
-        m.sincos_pre = 0;
-#endif
         // padding-row positions go to LDS unless that costs a workgroup per CU the launch
         // would use: one rollout launch has K_loc + 1 workgroups over the device's CUs
         const size_t stat = rollout_static_lds();
@@ -1271,9 +1246,6 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
                      rollout_blocks_per_cu(with_pad) >= std::min(need, rollout_blocks_per_cu(without))) ? 1 : 0;
         const size_t lds = rollout_lds_bytes(m, m.pad_lds) + stat;
         m.phased_lds = (int)rollout_phased_lds_bytes(m);
-#ifdef NO_PHASED_ROLLOUT
-        m.phased_lds = 0;
-#endif
         if (getenv("STOMP_DEBUG_PHASED")) fprintf(stderr, "stomp: phased rollout LDS %d B\n", m.phased_lds);
         if (lds > kRolloutLdsMax)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
@@ -2570,7 +2542,7 @@ int stomp_group_create(stomp_engine* const* engines, int32_t n, stomp_group** ou
         if (e->J != e0->J || e->N != e0->N || e->K != e0->K || e->S != e0->S ||
             rollout_lds_bytes(e->model, e->model.pad_lds) != lds0)
             return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model)");
-        if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->pre_host != 1 || e->terms_on ||
+        if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->terms_on ||
             e->split_modes || e->gather || e->use_cum || e->J > 16)
             return gfail(nullptr, STOMP_E_UNSUPPORTED,
                          "groups run single-device engines without reuse, state-cost terms or cumulative costs");

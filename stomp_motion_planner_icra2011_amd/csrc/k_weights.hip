@@ -58,10 +58,6 @@ __host__ __device__ inline size_t weights_rows_v_bytes(int K_loc, int tcw)
     return ((size_t)K_loc * tcw + (size_t)((K_loc + kSumBlock - 1) / kSumBlock) * kVPad) * sizeof(double);
 }
 
-#ifndef WEIGHTS_ROWS_BLOCK
-#define WEIGHTS_ROWS_BLOCK 256
-#endif
-constexpr int kWRB = WEIGHTS_ROWS_BLOCK;   // threads of a rows-kernel workgroup
 
 // EPT: cost-tile elements per lane, K_loc * TC <= EPT * 256
 template <int EPT>
@@ -246,10 +242,10 @@ __global__ __launch_bounds__(256) void k_weights(WeightArgs a)
 // rs, rs + RS, ... of column cc in registers.  Same phases, modes and canonical sums as
 // k_weights.
 // the body of k_weights_rows for tile block bid of nt; V = [K_loc][TCW] dynamic LDS
-template <int TCW, int EPT>
+template <int BLOCK, int TCW, int EPT>
 __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int nt, double* V)
 {
-    constexpr int BLOCK = kWRB, RS = BLOCK / TCW;
+    constexpr int RS = BLOCK / TCW;
     __shared__ double red0[BLOCK], red1[BLOCK];
     __shared__ double part[BLOCK];
     __shared__ double ps_s[TCW];
@@ -425,127 +421,73 @@ __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int n
     STAMP(5);
 }
 
-template <int TCW, int EPT>
-__global__ __launch_bounds__(kWRB) void k_weights_rows(WeightArgs a)
+template <int BLOCK, int TCW, int EPT>
+__global__ __launch_bounds__(BLOCK) void k_weights_rows(WeightArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double V[];   // [K_loc][TCW]
-    weights_rows<TCW, EPT>(a, blockIdx.x, gridDim.x, V);
+    weights_rows<BLOCK, TCW, EPT>(a, blockIdx.x, gridDim.x, V);
 }
 
 // the weights tiles of a group of engines in one launch (engine p's nt tiles at p nt)
-template <int TCW, int EPT>
-__global__ __launch_bounds__(kWRB) void k_weights_rows_group(const WeightArgs* as, int nt)
+template <int BLOCK, int TCW, int EPT>
+__global__ __launch_bounds__(BLOCK) void k_weights_rows_group(const WeightArgs* as, int nt)
 {
     extern __shared__ __attribute__((aligned(16))) double V[];
     const int p = blockIdx.x / nt;
-    weights_rows<TCW, EPT>(as[p], blockIdx.x - p * nt, nt, V);
-}
-
-// The same launch also carries k_pregen's rows for the next iteration (blocks nw on): the
-// weights tiles occupy under 256 workgroups, so the theta-independent noise of iteration
-// it + 1 (normals, sigma L z, M eps; noise_device.h) fills the idle CUs in the same dispatch
-// instead of waiting for the next rollout launch.  Those blocks ignore the stop flag (their
-// rows stay valid whatever the optimize loop decides).
-template <int TCW, int EPT>
-__global__ __launch_bounds__(256) void k_weights_rows_pre(WeightArgs a, NoiseArgs na, int nw)
-{
-    extern __shared__ __attribute__((aligned(16))) double V[];
-    if ((int)blockIdx.x < nw) {
-        weights_rows<TCW, EPT>(a, blockIdx.x, nw, V);
-        return;
-    }
-    const RolloutLds L = rollout_lds(na.J, na.N, 0, 0, 0, 0, 0, 0, 0);
-    double* zA = V;
-    double* zB = (double*)((unsigned char*)V + (L.nzB - L.nzA));
-    const int r = blockIdx.x - nw;
-    rollout_normals<256>(na, r, zA, zB, threadIdx.x);
-    if (na.J <= 8) {
-        pregen_eps_ng<256, 2>(na, r, zA, zB, threadIdx.x);
-        pregen_meps_ng<256, 2>(na, r, zB, threadIdx.x);
-    } else {
-        pregen_eps_ng<256, 4>(na, r, zA, zB, threadIdx.x);
-        pregen_meps_ng<256, 4>(na, r, zB, threadIdx.x);
-    }
+    weights_rows<BLOCK, TCW, EPT>(as[p], blockIdx.x - p * nt, nt, V);
 }
 
 STOMP_STAMP_ACCESSORS(weights)
 
-// columns per workgroup: as many as keep K_loc * TC <= 2048 (more workgroups, shorter
-// per-lane chains); K_loc in (2048, 4096] runs one column per workgroup with EPT = 16
-#ifndef WEIGHTS_TILE_ELEMS
-#define WEIGHTS_TILE_ELEMS 2048
-#endif
+// columns per workgroup of the column-tile kernel (k_weights, the fallback past the row tiles): as
+// many as keep K_loc * TC <= 2048
 int weights_tile(int K_loc)
 {
     int tc = 16;
-    while (tc > 1 && (size_t)K_loc * tc > WEIGHTS_TILE_ELEMS) tc >>= 1;
+    while (tc > 1 && (size_t)K_loc * tc > 2048) tc >>= 1;
     return tc;
 }
 
-#ifndef WEIGHTS_ROWS_TCW
-#define WEIGHTS_ROWS_TCW 4
-#endif
-template <int EPT>
-static void launch_rows(const WeightArgs& a, const NoiseArgs* pre, hipStream_t s)
+// Row tiles of four flat columns.  K_loc <= 1024: 512-lane workgroups (four or eight rows per
+// lane: the exp / division phases are per-lane chains, so more lanes finish them sooner; 12.5 ->
+// 11.5 us at cfg2 against 256 lanes); larger K_loc: 256 lanes with up to 32 rows per lane, and
+// for K_loc in (2048, 4096] two flat columns per workgroup so a lane's 32 rows still fit its
+// registers (the whole K = 4096 of cfg3 on one device; the one-column k_weights tiles read a
+// separate line per row there).  0 columns: the shape fits no row tile.
+static int rows_tcw(int K_loc)
 {
-    constexpr int TCW = WEIGHTS_ROWS_TCW;
-    const int JN = a.J * a.N;
-    const int nw = (JN + TCW - 1) / TCW;
-    size_t lds = weights_rows_v_bytes(a.K_loc, TCW);
-    if (pre) {
-        const RolloutLds L = rollout_lds(pre->J, pre->N, 0, 0, 0, 0, 0, 0, 0);
-        const size_t lp = 2 * (size_t)(L.nzB - L.nzA);
-        if (lp > lds) lds = lp;
-        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_pre<TCW, EPT>, lds);
-        hipLaunchKernelGGL((k_weights_rows_pre<TCW, EPT>), dim3(nw + pre->K_loc), dim3(256), lds, s, a, *pre, nw);
-        return;
-    }
-    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows<TCW, EPT>, lds);
-    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(kWRB), lds, s, a);
-}
-
-bool weights_carry_pregen(int K_loc)
-{
-#ifndef WEIGHTS_COLUMN_TILES
-    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
     const int nb = (K_loc + kSumBlock - 1) / kSumBlock;
-    return kWRB == 256 && nb * WEIGHTS_ROWS_TCW <= 256 && K_loc <= 32 * RS;
-#else
-    return false;
-#endif
+    if (K_loc <= 32 * 64 && nb * 4 <= 256) return 4;
+    if (K_loc <= 32 * 128 && nb * 2 <= 256) return 2;
+    return 0;
 }
 
-// half-width row tiles for K_loc in (32 RS, 64 RS]: two flat columns per workgroup, so a lane's
-// 32 rows still fit its registers (the whole K = 4096 of cfg3 on one device; the one-column
-// k_weights tiles read a separate line per row there)
-template <int EPT>
-static void launch_rows2(const WeightArgs& a, hipStream_t s)
+template <int BLOCK, int TCW, int EPT>
+static void launch_rows_t(const WeightArgs& a, hipStream_t s)
 {
-    constexpr int TCW = 2;
     const int nw = (a.J * a.N + TCW - 1) / TCW;
     const size_t lds = weights_rows_v_bytes(a.K_loc, TCW);
-    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows<TCW, EPT>, lds);
-    hipLaunchKernelGGL((k_weights_rows<TCW, EPT>), dim3(nw), dim3(kWRB), lds, s, a);
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows<BLOCK, TCW, EPT>, lds);
+    hipLaunchKernelGGL((k_weights_rows<BLOCK, TCW, EPT>), dim3(nw), dim3(BLOCK), lds, s, a);
 }
 
-void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre)
+void launch_weights(const WeightArgs& a, hipStream_t s)
 {
-#ifndef WEIGHTS_COLUMN_TILES
-    // row-coalesced flat-column tiles while a lane's rows fit its registers
-    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
-    const int nb = (a.K_loc + kSumBlock - 1) / kSumBlock;
-    if (nb * WEIGHTS_ROWS_TCW <= kWRB && (kWRB == 256 || !pre)) {
-        if (a.K_loc <= 4 * RS) return launch_rows<4>(a, pre, s);
-        if (a.K_loc <= 8 * RS) return launch_rows<8>(a, pre, s);
-        if (a.K_loc <= 16 * RS) return launch_rows<16>(a, pre, s);
-        if (a.K_loc <= 32 * RS) return launch_rows<32>(a, pre, s);
+    const int K = a.K_loc;
+    switch (rows_tcw(K)) {
+    case 4:
+        if (K <= 4 * 128) return launch_rows_t<512, 4, 4>(a, s);
+        if (K <= 8 * 128) return launch_rows_t<512, 4, 8>(a, s);
+        if (K <= 16 * 64) return launch_rows_t<256, 4, 16>(a, s);
+        return launch_rows_t<256, 4, 32>(a, s);
+    case 2:
+        return launch_rows_t<256, 2, 32>(a, s);
+    default:
+        break;
     }
-    if (!pre && kWRB == 256 && nb * 2 <= kWRB && a.K_loc <= 32 * (kWRB / 2)) return launch_rows2<32>(a, s);
-#endif
-    if (pre) launch_pregen(*pre, pre->K_loc, s);   // not reached: the engine checks weights_carry_pregen
     dim3 grid((a.N + a.tc - 1) / a.tc, a.J);
     const size_t lds = (size_t)a.K_loc * a.tc * sizeof(double);
-    if ((size_t)a.K_loc * a.tc <= 2048 && WEIGHTS_TILE_ELEMS <= 2048)
+    if ((size_t)a.K_loc * a.tc <= 2048)
         hipLaunchKernelGGL((k_weights<8>), grid, dim3(256), lds, s, a);
     else
         hipLaunchKernelGGL((k_weights<16>), grid, dim3(256), lds, s, a);
@@ -702,35 +644,29 @@ void launch_update_group(int J, int N, const UpdateArgs* as, int engines, hipStr
     if (engines > 0) hipLaunchKernelGGL(k_update_group, dim3(J * engines), dim3(256), 0, s, J, N, as);
 }
 
-// the rows path of launch_weights for a group (the engine checks rows_tiles() > 0)
+// the rows path of launch_weights for a group (the engine checks weights_group_tiles() > 0)
 int weights_group_tiles(int J, int N, int K_loc)
 {
-    constexpr int RS = kWRB / WEIGHTS_ROWS_TCW;
-    const int nb = (K_loc + kSumBlock - 1) / kSumBlock;
-    if (!(nb * WEIGHTS_ROWS_TCW <= kWRB) || K_loc > 32 * RS) return 0;
-    return (J * N + WEIGHTS_ROWS_TCW - 1) / WEIGHTS_ROWS_TCW;
+    if (rows_tcw(K_loc) != 4) return 0;
+    return (J * N + 3) / 4;
+}
+
+template <int BLOCK, int EPT>
+static void launch_rows_group_t(const WeightArgs* as, int engines, int nt, int K_loc, hipStream_t s)
+{
+    const size_t lds = weights_rows_v_bytes(K_loc, 4);
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<BLOCK, 4, EPT>, lds);
+    hipLaunchKernelGGL((k_weights_rows_group<BLOCK, 4, EPT>), dim3(nt * engines), dim3(BLOCK), lds, s, as, nt);
 }
 
 void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K_loc, hipStream_t s)
 {
-    constexpr int TCW = WEIGHTS_ROWS_TCW, RS = kWRB / TCW;
     const int nt = weights_group_tiles(J, N, K_loc);
     if (nt <= 0 || engines <= 0) return;
-    const size_t lds = weights_rows_v_bytes(K_loc, TCW);
-    const dim3 grid(nt * engines);
-    if (K_loc <= 4 * RS) {
-        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 4>, lds);
-        hipLaunchKernelGGL((k_weights_rows_group<TCW, 4>), grid, dim3(kWRB), lds, s, as, nt);
-    } else if (K_loc <= 8 * RS) {
-        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 8>, lds);
-        hipLaunchKernelGGL((k_weights_rows_group<TCW, 8>), grid, dim3(kWRB), lds, s, as, nt);
-    } else if (K_loc <= 16 * RS) {
-        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 16>, lds);
-        hipLaunchKernelGGL((k_weights_rows_group<TCW, 16>), grid, dim3(kWRB), lds, s, as, nt);
-    } else {
-        if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<TCW, 32>, lds);
-        hipLaunchKernelGGL((k_weights_rows_group<TCW, 32>), grid, dim3(kWRB), lds, s, as, nt);
-    }
+    if (K_loc <= 4 * 128) return launch_rows_group_t<512, 4>(as, engines, nt, K_loc, s);
+    if (K_loc <= 8 * 128) return launch_rows_group_t<512, 8>(as, engines, nt, K_loc, s);
+    if (K_loc <= 16 * 64) return launch_rows_group_t<256, 16>(as, engines, nt, K_loc, s);
+    return launch_rows_group_t<256, 32>(as, engines, nt, K_loc, s);
 }
 
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,

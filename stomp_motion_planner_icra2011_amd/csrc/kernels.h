@@ -316,11 +316,7 @@ int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS a
 constexpr size_t kLdsPerCu = 144 * 1024;
 constexpr size_t kRolloutLdsMax = 156 * 1024;                // dynamic + static per workgroup
 void launch_cumulative(const WeightArgs& a, double* cum, hipStream_t s);
-// pre: also make the next iteration's k_pregen rows in the same launch (weights_carry_pregen)
-void launch_weights(const WeightArgs& a, hipStream_t s, const NoiseArgs* pre = nullptr);
-bool weights_carry_pregen(int K_loc);
-// where the next iteration's pregen rows ride: 1 = the rollout launch (low-priority blocks),
-// 2 = the weights launch (STOMP_PREGEN_HOST=weights)
+void launch_weights(const WeightArgs& a, hipStream_t s);
 int weights_tile(int K_loc);
 // theta += M u; with delta: delta = M u and theta untouched
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total,
