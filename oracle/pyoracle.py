@@ -194,10 +194,10 @@ def _arr(vals, T):
 class Oracle:
     """One planning problem on the CPU oracle (keeps every buffer it points at alive)."""
 
-    def __init__(self, problem, dense: bool = False, threads: int = 1, sum_block: int = 64, ref_arith: bool = False):
-        """dense: the reference's dense N x N products (CPU baseline structure); ref_arith: the
+    def __init__(self, problem, dense: bool = False, threads: int = 1, sum_block: int = 64, ref_arith: int = 0):
+        """dense: the reference's dense N x N products (CPU baseline structure); ref_arith 1: the
         reference's written arithmetic order (non-fused L z / M eps, sequential rollout sums)
-        instead of the engine's contract."""
+        instead of the engine's contract; 2: also Eigen 2's two-lane packet VectorXd::sum()."""
         L = lib()
         p = problem
         self.problem = p

@@ -17,8 +17,11 @@
  * written order everywhere: L z and M eps non-fused and k ascending over the dense matrix
  * (multivariate_gaussian.h:93, policy_improvement.cpp:477), and the rollout sums of P and
  * eps * P sequential over all K (policy_improvement.cpp:352-358, 376-379).
- * tests/test_reference_order.py measures how far the engine contract drifts from it on the
- * north-star quantity (best_group_trajectory_).
+ * cfg.ref_arith = 2 also sums VectorXd::sum() (Rollout::getCost, policy_improvement.cpp:149-156;
+ * last_trajectory_cost_ = costs.sum(), stomp_optimizer.cpp:1155) as Eigen 2's SSE2 packet
+ * reduction would: two interleaved lanes, then their sum (vec_sum).
+ * tests/test_reference_order.py measures how far the engine contract drifts from them on the
+ * north-star quantity (best_group_trajectory_) and on the discrete decisions.
  */
 #include "stomp_oracle.h"
 #include "dmath.h"
@@ -1059,6 +1062,8 @@ static void handle_joint_limits(const so_problem* P, double* traj)
     }
 }
 
+static double vec_sum(const so_problem* P, const double* x, int n);
+
 static void execute_one(const so_problem* P, exec_scratch* sc, const double* params, double* costs,
                         int* collision_free, double* traj_out, int iteration_member, double* total, int* cons_ok)
 {
@@ -1121,7 +1126,7 @@ static void execute_one(const so_problem* P, exec_scratch* sc, const double* par
                    P->cfg.torque_cost_weight * tq;
         costs[i - SO_PAD] = c;
     }
-    for (int t = 0; t < N; ++t) sum = (t == 0) ? costs[0] : sum + costs[t];   /* costs.sum() :1155 */
+    sum = vec_sum(P, costs, N);   /* costs.sum() :1155 */
     *collision_free = cf;
     if (cons_ok) *cons_ok = cs;
     if (total) *total = sum;
@@ -1230,17 +1235,32 @@ static void matvec(const double* A, int n, const double* x, double* y, int lower
     }
 }
 
+/* VectorXd::sum().  ref_arith 2: Eigen 2's SSE2 packet reduction (third party, unpinned: two
+ * double lanes over the 16-byte-aligned data, lane k summing x[k], x[k + 2], ..., then lane 0 +
+ * lane 1, then the odd last element); otherwise index order. */
+static double vec_sum(const so_problem* P, const double* x, int n)
+{
+    if (P->cfg.ref_arith == 2 && n >= 2) {
+        double l0 = x[0], l1 = x[1];
+        int i = 2;
+        for (; i + 1 < n; i += 2) {
+            l0 += x[i];
+            l1 += x[i + 1];
+        }
+        double r = l0 + l1;
+        for (; i < n; ++i) r += x[i];
+        return r;
+    }
+    double s = x[0];
+    for (int t = 1; t < n; ++t) s += x[t];
+    return s;
+}
+
 /* Rollout::getCost (policy_improvement.cpp:149-156) */
 static double rollout_cost(const so_problem* P, const double* state, const double* ctrl)
 {
-    double c = state[0];
-    for (int t = 1; t < P->N; ++t) c += state[t];
-    for (int d = 0; d < P->J; ++d) {
-        const double* x = ctrl + (size_t)d * P->N;
-        double s = x[0];
-        for (int t = 1; t < P->N; ++t) s += x[t];
-        c += s;
-    }
+    double c = vec_sum(P, state, P->N);
+    for (int d = 0; d < P->J; ++d) c += vec_sum(P, ctrl + (size_t)d * P->N, P->N);
     return c;
 }
 

@@ -127,7 +127,8 @@ typedef struct {
     int num_orientation_constraints;
     const so_orientation_constraint* orientation_constraints;
     /* 1: the reference's written arithmetic order: non-fused dense L z / M eps and sequential
-     * rollout sums over all K (instead of the engine's fma chain and 64-rollout blocks) */
+     * rollout sums over all K (instead of the engine's fma chain and 64-rollout blocks);
+     * 2: also VectorXd::sum() as Eigen 2's two-lane SSE2 packet reduction */
     int ref_arith;
 } so_config;
 

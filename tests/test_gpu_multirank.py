@@ -186,3 +186,41 @@ def test_ranks_disagreeing_on_the_decomposition_fail(monkeypatch):
     with pytest.raises(RuntimeError, match="differs from the group"):
         eng.Engine(p, rank=1, world_size=2, comm_id=gid)
     del e0
+
+
+def test_cfg3_eight_rank_split_bitwise():
+    # cfg3's real 8-GPU decomposition (BASELINE configs[2]): K = 4096 over 8 ranks, K_loc = 512,
+    # N = 199, 256^3 device-built field, partials mode (its 6.5 MB of state rows are past gather
+    # mode's 1 MiB), three iterations; every rank's slice of the oracle's rows bit for bit
+    p = pb.make_problem(dof=7, waypoints=200, grid_n=256, num_rollouts=4096, num_reused_rollouts=0,
+                        build_grid=False)
+    n = p.grid.n
+    buf = eng.DeviceBuffer(2 * n ** 3)
+    eng.sdf_build_device(p, buf.ptr)
+    p.sdf = buf.to_numpy(np.uint16, (n, n, n))
+    gid = eng.comm_local_id(8)
+    engines = [eng.Engine(p, rank=r, world_size=8, comm_id=gid, sdf_device_ptr=buf.ptr) for r in range(8)]
+    assert all(e.shard_mode == "partials" and e.K_loc == 512 for e in engines)
+    o = po.Oracle(p, threads=THREADS)
+
+    def drive(r, e):
+        rec = []
+        for it in (1, 2, 3):
+            c = e.iterate(it)
+            rec.append((c, e.theta(), e.last_trajectory(), e.rollouts("state_costs"), e.rollouts("probabilities")))
+        return rec
+
+    recs = on_threads(engines, drive)
+    for k, it in enumerate((1, 2, 3)):
+        oc = o.iterate(it)
+        st, pr = o.rollouts("state_costs"), o.rollouts("probabilities")
+        for r in range(8):
+            c, th, last, est, epr = recs[r][k]
+            assert c == oc, (it, r)
+            np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it} rank {r}")
+            np.testing.assert_array_equal(last, o.last_trajectory())
+            np.testing.assert_array_equal(est, st[512 * r:512 * (r + 1)], err_msg=f"state it {it} rank {r}")
+            np.testing.assert_array_equal(epr, pr[512 * r:512 * (r + 1)], err_msg=f"prob it {it} rank {r}")
+    for e in engines:
+        e.close()
+    buf.free()
