@@ -17,14 +17,16 @@
 //     (StompRobotModel, StompCollisionSpace); orientation path constraints arrive as
 //     Constraints; the ROS publishers are not taken (no visualisation)
 //   * when the policy is a StompOptimizer's, the rollouts, the policy parameters and the
-//     PolicyImprovement state live in HBM inside its engine (the counts fixed when the engine is
-//     created); any other Policy, or rollout counts other than the engine's (setNumRollouts),
-//     runs PolicyImprovement on the host with the same arithmetic and noise stream
+//     PolicyImprovement state live in HBM: in the optimizer's engine for its own counts, or, for
+//     other counts (setNumRollouts) or another use_cumulative_costs, in a second engine of the
+//     same problem on the same device; any other Policy (or more than one extra rollout) runs
+//     PolicyImprovement on the host with the same arithmetic and noise stream
 // Failures return false and leave the reason in lastError() (the reference logs with
 // ROS_ERROR and returns false).  One optimizer owns one engine (one HIP device stream).
 #ifndef STOMP_MOTION_PLANNER_STOMP_FACADE_H
 #define STOMP_MOTION_PLANNER_STOMP_FACADE_H
 
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -46,7 +48,65 @@ struct MatrixXd {
     int cols() const { return cols_; }
     double& operator()(int r, int c) { return data_[(size_t)r * cols_ + c]; }
     double operator()(int r, int c) const { return data_[(size_t)r * cols_ + c]; }
+    void resize(int r, int c)
+    {
+        rows_ = r;
+        cols_ = c;
+        data_.assign((size_t)r * c, 0.0);
+    }
 };
+
+namespace detail {
+template <class M>
+MatrixXd to_mat(const M& m)
+{
+    MatrixXd o((int)m.rows(), (int)m.cols());
+    for (int r = 0; r < o.rows(); ++r)
+        for (int c = 0; c < o.cols(); ++c) o(r, c) = m(r, c);
+    return o;
+}
+template <class M>
+void from_mat(const MatrixXd& s, M& m)
+{
+    m.resize(s.rows(), s.cols());
+    for (int r = 0; r < s.rows(); ++r)
+        for (int c = 0; c < s.cols(); ++c) m(r, c) = s(r, c);
+}
+}  // namespace detail
+
+// Eigen-shaped arguments.  The reference's Task / Policy / PolicyImprovement calls pass
+// Eigen::VectorXd and Eigen::MatrixXd; the template overloads below take any vector type with
+// size(), data() and resize(n) (Eigen::VectorXd, std::vector<double>) and any matrix type with
+// rows(), cols(), resize(r, c) and operator()(r, c) (Eigen::MatrixXd), so the node's calls compile
+// unchanged against this header, which does not include Eigen.  The std::vector overloads are the
+// exact matches for this header's own types.
+namespace detail {
+template <class V>
+VectorXd to_vec(const V& v)
+{
+    return VectorXd(v.data(), v.data() + v.size());
+}
+template <class V>
+void from_vec(const VectorXd& s, V& v)
+{
+    v.resize(s.size());
+    std::copy(s.begin(), s.end(), v.data());
+}
+template <class V>
+std::vector<VectorXd> to_vecs(const std::vector<V>& v)
+{
+    std::vector<VectorXd> o;
+    o.reserve(v.size());
+    for (const V& x : v) o.push_back(to_vec(x));
+    return o;
+}
+template <class V>
+void from_vecs(const std::vector<VectorXd>& s, std::vector<V>& v)
+{
+    v.resize(s.size());
+    for (size_t i = 0; i < s.size(); ++i) from_vec(s[i], v[i]);
+}
+}  // namespace detail
 
 // config/params.yaml + StompParameters (stomp_parameters.cpp:50-76)
 struct StompParameters {
@@ -151,6 +211,27 @@ public:
                              const std::vector<VectorXd>& noise, const double weight,
                              std::vector<VectorXd>& control_costs) override;
     StompOptimizer* owner() const { return owner_; }
+    // Eigen-shaped forms (see detail::): parameters [J] of N, updates [J] of N x N (row 0 used)
+    template <class V>
+    bool getParameters(std::vector<V>& parameters)
+    {
+        std::vector<VectorXd> p;
+        if (!getParameters(p)) return false;
+        detail::from_vecs(p, parameters);
+        return true;
+    }
+    template <class V>
+    bool setParameters(const std::vector<V>& parameters)
+    {
+        return setParameters(detail::to_vecs(parameters));
+    }
+    template <class M>
+    bool updateParameters(const std::vector<M>& updates)
+    {
+        std::vector<MatrixXd> u;
+        for (const M& m : updates) u.push_back(detail::to_mat(m));
+        return updateParameters(u);
+    }
 
 private:
     bool loadDifferentiation();
@@ -192,6 +273,18 @@ public:
     StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model, const StompParameters* parameters,
                    StompCollisionSpace* collision_space, const Constraints& constraints = Constraints(),
                    int device = 0, void* stream = nullptr);
+    // the planner node's call shape (stomp_planner_node.cpp:228-230: trajectory, robot model,
+    // planning group, parameters, the visualisation / marker / statistics publishers, collision
+    // space, path constraints): the group and the publishers are taken and ignored (the robot
+    // model passed here is already the planning group's; nothing is visualised)
+    template <class Group, class Publisher>
+    StompOptimizer(StompTrajectory* trajectory, const StompRobotModel* robot_model, const Group* /*planning_group*/,
+                   const StompParameters* parameters, const Publisher& /*vis_marker_array_publisher*/,
+                   const Publisher& /*vis_marker_publisher*/, const Publisher& /*stats_publisher*/,
+                   StompCollisionSpace* collision_space, const Constraints& constraints = Constraints())
+        : StompOptimizer(trajectory, robot_model, parameters, collision_space, constraints)
+    {
+    }
     ~StompOptimizer() override;
     StompOptimizer(const StompOptimizer&) = delete;
     StompOptimizer& operator=(const StompOptimizer&) = delete;
@@ -207,6 +300,20 @@ public:
     bool getPolicy(std::shared_ptr<Policy>& policy) override;
     bool setPolicy(const std::shared_ptr<Policy> policy) override;
     bool getControlCostWeight(double& control_cost_weight) override;
+    // Task::execute with Eigen-shaped vectors (task.h:70)
+    template <class V>
+    bool execute(std::vector<V>& parameters, V& costs, const int iteration_number)
+    {
+        std::vector<VectorXd> p = detail::to_vecs(parameters);
+        VectorXd c;
+        if (!execute(p, c, iteration_number)) return false;
+        detail::from_vec(c, costs);
+        return true;
+    }
+    // the reference's setSharedPtr / resetSharedPtr (stomp_optimizer.cpp:1202-1210): the loop here
+    // holds no owning pointer to its task, so these are no-ops kept for the node's call sequence
+    void setSharedPtr(const std::shared_ptr<StompOptimizer>& /*self*/) {}
+    void resetSharedPtr() {}
 
     // batched Task::execute: parameters [E][J] N -> costs [E] N (one engine launch)
     bool executeBatch(std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
@@ -234,8 +341,14 @@ private:
     friend class PolicyImprovement;
     friend class CovariantTrajectoryPolicy;
     bool check(int rc);
+    // an engine of the same problem with other rollout counts / cumulative-cost setting (the
+    // device rollout set of a PolicyImprovement that asks for them); nullptr and err on failure
+    stomp_engine* createSibling(int num_rollouts, int num_reused_rollouts, bool use_cumulative_costs,
+                                std::string& err) const;
     StompTrajectory* trajectory_;
     const StompParameters* parameters_;
+    stomp_engine_desc desc_{};          // the engine's descriptor (its tables are the caller's)
+    Constraints constraints_;           // desc_.orientation_constraints points here
     stomp_engine* engine_ = nullptr;
     std::shared_ptr<Policy> policy_;
     int J_ = 0, N_ = 0;
@@ -246,12 +359,14 @@ private:
     std::string error_;
 };
 
-// policy_improvement.h:65-126 / policy_improvement.cpp:64-489.  Two places the rollout set can
-// live, with the same results:
-//   * the engine of a StompOptimizer (stomp_pi_* of the C ABI) when the policy is that optimizer's
-//     CovariantTrajectoryPolicy and the counts are the engine's;
-//   * the host, for any other Policy, or after setNumRollouts asks for counts the engine was not
-//     created with: the reference's algorithm over the Policy interface (getControlCosts ->
+// policy_improvement.h:65-126 / policy_improvement.cpp:64-489.  Where the rollout set lives,
+// with the same results:
+//   * when the policy is a StompOptimizer's CovariantTrajectoryPolicy, on the device (stomp_pi_* of
+//     the C ABI): in that optimizer's engine for its own counts and use_cumulative_costs, else in
+//     a second engine of the same problem made for the requested counts / setting (initialize,
+//     setNumRollouts), whose theta is refreshed from the optimizer's before each getRollouts;
+//   * the host, for any other Policy or more than one extra rollout (the engine evaluates one
+//     noiseless extra rollout): the reference's algorithm over the Policy interface (getControlCosts ->
 //     R^-1, chol, projection; computeControlCosts; getParameters), with the engine's noise stream
 //     (Philox normals keyed by seed, iteration, dimension, rollout) and arithmetic contract (fma
 //     chains for L z and M eps, 64-rollout blocked sums, deterministic exp).
@@ -261,6 +376,8 @@ class PolicyImprovement {
 public:
     PolicyImprovement();
     ~PolicyImprovement();
+    PolicyImprovement(const PolicyImprovement&) = delete;
+    PolicyImprovement& operator=(const PolicyImprovement&) = delete;
     bool initialize(const int num_rollouts, const int num_time_steps, const int num_reused_rollouts,
                     const int num_extra_rollouts, std::shared_ptr<Policy> policy, bool use_cumulative_costs = true);
     // policy_improvement.cpp:96-147: new counts, the reuse state reset (the next getRollouts
@@ -275,6 +392,38 @@ public:
     // [J] N x N matrices, row 0 = the update (policy_improvement.cpp:370-383)
     bool improvePolicy(std::vector<MatrixXd>& parameter_updates);
     bool addExtraRollouts(std::vector<std::vector<VectorXd>>& rollouts, std::vector<VectorXd>& rollout_costs);
+    // the same four calls with Eigen-shaped vectors / matrices (policy_improvement.h:86-126)
+    template <class V>
+    bool getRollouts(std::vector<std::vector<V>>& rollouts, const std::vector<double>& noise_stddev)
+    {
+        std::vector<std::vector<VectorXd>> r;
+        if (!getRollouts(r, noise_stddev)) return false;
+        rollouts.resize(r.size());
+        for (size_t i = 0; i < r.size(); ++i) detail::from_vecs(r[i], rollouts[i]);
+        return true;
+    }
+    template <class M>
+    bool setRolloutCosts(const M& costs, const double control_cost_weight, std::vector<double>& rollout_costs_total)
+    {
+        return setRolloutCosts(detail::to_mat(costs), control_cost_weight, rollout_costs_total);
+    }
+    template <class M>
+    bool improvePolicy(std::vector<M>& parameter_updates)
+    {
+        std::vector<MatrixXd> u;
+        if (!improvePolicy(u)) return false;
+        parameter_updates.resize(u.size());
+        for (size_t i = 0; i < u.size(); ++i) detail::from_mat(u[i], parameter_updates[i]);
+        return true;
+    }
+    template <class V>
+    bool addExtraRollouts(std::vector<std::vector<V>>& rollouts, std::vector<V>& rollout_costs)
+    {
+        std::vector<std::vector<VectorXd>> r;
+        for (const auto& x : rollouts) r.push_back(detail::to_vecs(x));
+        std::vector<VectorXd> c = detail::to_vecs(rollout_costs);
+        return addExtraRollouts(r, c);
+    }
     // The noise of getRollouts is a counter-based stream keyed by an iteration number (the
     // reference's generators are stateful); each getRollouts uses the current key and advances
     // it by one, starting at 1.  PolicyImprovementLoop sets it to runSingleIteration's number.
@@ -282,8 +431,10 @@ public:
     // the noise key of the host rollout set (the engine's comes from StompParameters::seed;
     // a StompOptimizer's policy sets it from there)
     void setNoiseSeed(uint64_t seed) { seed_ = seed; }
-    // true while the rollout set lives in a StompOptimizer's engine
+    // true while the rollout set lives on the device (the optimizer's engine or one of its own)
     bool onEngine() const { return engine_ != nullptr && !host_; }
+    // true when that device rollout set is an engine of this PolicyImprovement's own (other counts)
+    bool onOwnEngine() const { return onEngine() && engine_ == own_; }
     const std::string& lastError() const { return error_; }
 
 private:
@@ -293,6 +444,7 @@ private:
     std::shared_ptr<Policy> policy_;
     StompOptimizer* owner_ = nullptr;
     stomp_engine* engine_ = nullptr;
+    stomp_engine* own_ = nullptr;       // the second engine (counts other than the optimizer's)
     std::shared_ptr<HostRollouts> host_;
     uint64_t seed_ = 0x53544F4D50000000ull;
     int J_ = 0, N_ = 0, K_ = 0, K_gen_ = 0, noise_iteration_ = 1;

@@ -94,8 +94,10 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
     d.torque_root = robot_model->torque_root;
     d.torque_tip = robot_model->torque_tip;
     for (int k = 0; k < 3; ++k) d.gravity[k] = robot_model->gravity[k];
-    d.num_orientation_constraints = (int32_t)constraints.orientation_constraints.size();
-    d.orientation_constraints = constraints.orientation_constraints.data();
+    constraints_ = constraints;
+    d.num_orientation_constraints = (int32_t)constraints_.orientation_constraints.size();
+    d.orientation_constraints = constraints_.orientation_constraints.data();
+    desc_ = d;
     int rc = stomp_engine_create(&d, &engine_);
     if (rc) {
         error_ = engine_error(nullptr, rc);
@@ -115,6 +117,26 @@ bool StompOptimizer::check(int rc)
     if (rc == 0) return true;
     error_ = engine_error(engine_, rc);
     return false;
+}
+
+stomp_engine* StompOptimizer::createSibling(int num_rollouts, int num_reused_rollouts, bool use_cumulative_costs,
+                                            std::string& err) const
+{
+    if (!engine_) {
+        err = "no engine";
+        return nullptr;
+    }
+    stomp_engine_desc d = desc_;
+    d.num_rollouts = num_rollouts;
+    d.num_reused_rollouts = num_reused_rollouts;
+    d.use_cumulative_costs = use_cumulative_costs ? 1 : 0;
+    stomp_engine* e = nullptr;
+    const int rc = stomp_engine_create(&d, &e);
+    if (rc) {
+        err = engine_error(nullptr, rc);
+        return nullptr;
+    }
+    return e;
 }
 
 bool StompOptimizer::optimize()
@@ -459,7 +481,10 @@ struct PolicyImprovement::HostRollouts {
 };
 
 PolicyImprovement::PolicyImprovement() = default;
-PolicyImprovement::~PolicyImprovement() = default;
+PolicyImprovement::~PolicyImprovement()
+{
+    if (own_) stomp_engine_destroy(own_);
+}
 
 bool PolicyImprovement::check(int rc)
 {
@@ -476,6 +501,10 @@ bool PolicyImprovement::initialize(const int num_rollouts, const int num_time_st
     host_.reset();
     owner_ = nullptr;
     engine_ = nullptr;
+    if (own_) {
+        stomp_engine_destroy(own_);
+        own_ = nullptr;
+    }
     if (!policy) {
         error_ = "PolicyImprovement::initialize: null policy";
         return false;
@@ -494,11 +523,6 @@ bool PolicyImprovement::initialize(const int num_rollouts, const int num_time_st
         if (num_time_steps != owner_->N_) {
             error_ = "PolicyImprovement::initialize: num_time_steps differs from the engine's";
             return false;
-        }
-        if (use_cumulative_costs != owner_->parameters_->use_cumulative_costs) {
-            // the engine's setting is fixed at creation: the rollout set moves to the host
-            if (!hostInitialize(num_rollouts, num_reused_rollouts, num_extra_rollouts)) return false;
-            return (initialized_ = true);
         }
     }
     if (!setNumRollouts(num_rollouts, num_reused_rollouts, num_extra_rollouts)) return false;
@@ -554,15 +578,31 @@ bool PolicyImprovement::setNumRollouts(const int num_rollouts, const int num_reu
         error_ = "setNumRollouts: negative or zero rollout count";
         return false;
     }
-    if (!host_) {
-        if (owner_ && num_rollouts == owner_->parameters_->num_rollouts &&
-            num_reused_rollouts == owner_->parameters_->num_reused_rollouts && num_extra_rollouts == 1) {
-            // the engine's own counts: its reuse state starts over on the next getRollouts
-            K_ = num_rollouts;
-            return engine_ ? check(stomp_pi_reset(engine_)) : true;
+    if (owner_ && num_extra_rollouts == 1) {
+        // on the device: the optimizer's engine for its own counts and setting (its reuse state
+        // starts over on the next getRollouts), else an engine of our own for the new ones
+        host_.reset();
+        if (own_) {
+            stomp_engine_destroy(own_);
+            own_ = nullptr;
         }
-        return hostInitialize(num_rollouts, num_reused_rollouts, num_extra_rollouts);
+        K_ = num_rollouts;
+        if (num_rollouts == owner_->parameters_->num_rollouts &&
+            num_reused_rollouts == owner_->parameters_->num_reused_rollouts &&
+            use_cumulative_ == owner_->parameters_->use_cumulative_costs) {
+            engine_ = owner_->engine_;
+            return check(stomp_pi_reset(engine_));
+        }
+        std::string err;
+        own_ = owner_->createSibling(num_rollouts, num_reused_rollouts, use_cumulative_, err);
+        engine_ = own_;
+        if (!own_) {
+            error_ = "setNumRollouts: " + err;
+            return false;
+        }
+        return true;
     }
+    if (!host_) return hostInitialize(num_rollouts, num_reused_rollouts, num_extra_rollouts);
     HostRollouts& h = *host_;
     h.K = num_rollouts;
     h.Kr = num_reused_rollouts;
@@ -582,6 +622,13 @@ bool PolicyImprovement::getRollouts(std::vector<std::vector<VectorXd>>& rollouts
     if (!initialized_) { error_ = "getRollouts: not initialized"; return false; }
     if ((int)noise_stddev.size() != J_) { error_ = "getRollouts: one noise_stddev per dimension"; return false; }
     if (!host_) {
+        if (engine_ == own_) {
+            // generateRollouts perturbs the policy's current parameters: the optimizer's theta
+            std::vector<double> th((size_t)J_ * N_);
+            if (!check(stomp_engine_get_theta(owner_->engine_, th.data())) ||
+                !check(stomp_engine_set_theta(own_, th.data())))
+                return false;
+        }
         std::vector<double> buf((size_t)K_ * J_ * N_);
         int32_t n = 0;
         if (!check(stomp_pi_get_rollouts(engine_, noise_iteration_, noise_stddev.data(), buf.data(), &n))) return false;

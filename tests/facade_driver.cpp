@@ -324,6 +324,30 @@ int run_loop(PolicyImprovementLoop& loop, StompOptimizer& opt, std::shared_ptr<P
 
 }  // namespace
 
+// Stand-ins with the member names of Eigen::VectorXd / Eigen::MatrixXd that the facade's template
+// overloads use (size, data, resize, operator()), and of the node's planning group / ROS
+// publisher arguments: the node's own calls, type-checked and run through the Eigen-shaped API
+struct EigenLikeVector {
+    std::vector<double> v;
+    long size() const { return (long)v.size(); }
+    const double* data() const { return v.data(); }
+    double* data() { return v.data(); }
+    void resize(long n) { v.assign((size_t)n, 0.0); }
+    double& operator()(long i) { return v[(size_t)i]; }
+    double operator()(long i) const { return v[(size_t)i]; }
+};
+struct EigenLikeMatrix {
+    long r = 0, c = 0;
+    std::vector<double> d;
+    long rows() const { return r; }
+    long cols() const { return c; }
+    void resize(long rr, long cc) { r = rr; c = cc; d.assign((size_t)(rr * cc), 0.0); }
+    double& operator()(long i, long j) { return d[(size_t)(i * c + j)]; }
+    double operator()(long i, long j) const { return d[(size_t)(i * c + j)]; }
+};
+struct NodePlanningGroup {};
+struct NodePublisher {};
+
 int main(int argc, char** argv)
 {
     if (argc < 4) {
@@ -481,6 +505,60 @@ int main(int argc, char** argv)
             for (const auto& row : theta) write_vec(out, row);
             write_vec(out, totals);
         }
+    } else if (mode == "pi_steps_eigen") {
+        // pi_steps with Eigen-shaped arguments and the node's constructor call shape
+        // (stomp_planner_node.cpp:228-234)
+        NodePlanningGroup group;
+        NodePublisher pub;
+        auto node_opt = std::make_shared<StompOptimizer>(&p.traj, &p.robot, &group, &p.params, pub, pub, pub, &p.space,
+                                                         Constraints());
+        node_opt->setSharedPtr(node_opt);
+        if (!node_opt->ok()) return 40;
+        std::shared_ptr<Policy> policy;
+        node_opt->getPolicy(policy);
+        auto* ctp = dynamic_cast<CovariantTrajectoryPolicy*>(policy.get());
+        PolicyImprovement pi;
+        const StompParameters& q = p.params;
+        if (!ctp || !pi.initialize(q.num_rollouts, p.traj.num_points, q.num_reused_rollouts, 1, policy,
+                                   q.use_cumulative_costs)) {
+            std::cerr << pi.lastError() << "\n";
+            return 41;
+        }
+        double w = 0.0;
+        node_opt->getControlCostWeight(w);
+        const int J = p.traj.num_joints, N = p.traj.num_points;
+        for (int it = 1; it <= 10; ++it) {
+            std::vector<double> noise(J);
+            for (int i = 0; i < J; ++i) noise[i] = q.noise_stddev[i] * std::pow(q.noise_decay[i], it - 1);
+            std::vector<std::vector<EigenLikeVector>> rollouts;
+            if (!pi.getRollouts(rollouts, noise)) { std::cerr << pi.lastError() << "\n"; return 42; }
+            EigenLikeMatrix costs;
+            costs.resize(q.num_rollouts, N);
+            for (size_t r = 0; r < rollouts.size(); ++r) {
+                EigenLikeVector c;
+                if (!node_opt->execute(rollouts[r], c, it)) return 43;
+                for (int t = 0; t < N; ++t) costs((long)r, t) = c(t);
+            }
+            std::vector<double> totals;
+            std::vector<EigenLikeMatrix> updates;
+            if (!pi.setRolloutCosts(costs, w, totals) || !pi.improvePolicy(updates)) {
+                std::cerr << pi.lastError() << "\n";
+                return 44;
+            }
+            if (!ctp->updateParameters(updates)) return 45;
+            std::vector<EigenLikeVector> theta;
+            ctp->getParameters(theta);
+            EigenLikeVector c;
+            if (!node_opt->execute(theta, c, it)) return 46;
+            std::vector<std::vector<EigenLikeVector>> extra(1, theta);
+            std::vector<EigenLikeVector> extra_cost(1, c);
+            if (!pi.addExtraRollouts(extra, extra_cost)) { std::cerr << pi.lastError() << "\n"; return 47; }
+            std::fprintf(out, "%.17g %d %zu\n", node_opt->lastTrajectoryCost(),
+                         node_opt->lastTrajectoryCollisionFree() ? 1 : 0, rollouts.size());
+            for (const auto& row : theta) write_vec(out, row.v);
+            write_vec(out, totals);
+        }
+        node_opt->resetSharedPtr();
     } else if (mode == "pi_user") {
         auto policy = std::make_shared<UserPolicy>(*opt, p.traj, p.params);
         if (!policy->ok()) return 23;
@@ -492,21 +570,26 @@ int main(int argc, char** argv)
         }
         if (int rc = run_loop(loop, *opt, policy, out)) return rc;
     } else if (mode == "pi_setnum") {
+        // input: K_r for setNumRollouts, and 1 to initialize with the other use_cumulative_costs
+        // than the optimizer's (policy_improvement.cpp:64-147): either way the rollout set stays
+        // on the device, in an engine of the PolicyImprovement's own
         if (argc < 6) return 2;
-        int kr = 0;
+        int kr = 0, flip = 0;
         std::ifstream f(argv[5]);
-        f >> kr;
+        f >> kr >> flip;
         if (!f) return 2;
         std::shared_ptr<Policy> policy;
         opt->getPolicy(policy);
         PolicyImprovement pi;
         const StompParameters& q = p.params;
-        if (!pi.initialize(q.num_rollouts, p.traj.num_points, q.num_reused_rollouts, 1, policy, q.use_cumulative_costs) ||
-            !pi.onEngine()) {
-            std::cerr << pi.lastError() << "\n";
+        const bool cum = flip ? !q.use_cumulative_costs : q.use_cumulative_costs;
+        if (!pi.initialize(q.num_rollouts, p.traj.num_points, q.num_reused_rollouts, 1, policy, cum) ||
+            !pi.onEngine() || pi.onOwnEngine() != (flip != 0)) {
+            std::cerr << "initialize: " << pi.lastError() << "\n";
             return 25;
         }
-        if (!pi.setNumRollouts(q.num_rollouts, kr, 1) || pi.onEngine()) {
+        if (!pi.setNumRollouts(q.num_rollouts, kr, 1) || !pi.onEngine() ||
+            pi.onOwnEngine() != (flip != 0 || kr != q.num_reused_rollouts)) {
             std::cerr << "setNumRollouts: " << pi.lastError() << "\n";
             return 26;
         }

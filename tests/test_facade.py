@@ -89,14 +89,17 @@ def _getcost(state, control):
 
 
 @pytest.mark.gpu
-def test_facade_policy_improvement_steps(tmp_path):
+@pytest.mark.parametrize("mode", ["pi_steps", "pi_steps_eigen"])
+def test_facade_policy_improvement_steps(tmp_path, mode):
     # PolicyImprovement / Policy / Task driven by hand (policy_improvement_loop.cpp:143-202):
-    # theta and the noiseless cost of every iteration, and the setRolloutCosts totals
+    # theta and the noiseless cost of every iteration, and the setRolloutCosts totals.
+    # pi_steps_eigen: the same calls with Eigen-shaped vectors / matrices (stand-ins with Eigen's
+    # member names) and the optimizer built by the node's own constructor call shape
     p = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=4)
     prob, sdf = fu.write_problem(p, str(tmp_path))
     exe = fu.build_driver(str(tmp_path))
     res = str(tmp_path / "out.txt")
-    r = subprocess.run([exe, prob, sdf, "pi_steps", res], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([exe, prob, sdf, mode, res], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
     toks = open(res).read().split()
     o = po.Oracle(p)
@@ -203,19 +206,23 @@ def test_facade_user_policy_matches_oracle(tmp_path):
 
 
 @pytest.mark.gpu
-def test_facade_set_num_rollouts_moves_to_host(tmp_path):
-    # setNumRollouts with a K_r the engine was not created with (policy_improvement.cpp:96-147):
-    # the rollout set continues on the host, bit for bit the oracle configured with that K_r
+@pytest.mark.parametrize("kr,flip", [(7, 0), (4, 1), (7, 1)])
+def test_facade_set_num_rollouts_stays_on_device(tmp_path, kr, flip):
+    # setNumRollouts with a K_r the engine was not created with (policy_improvement.cpp:96-147),
+    # and / or initialize with the other use_cumulative_costs (:64-94): the rollout set stays on
+    # the device (an engine of the PolicyImprovement's own, onOwnEngine), bit for bit the oracle
+    # configured with that K_r and setting
     p = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=4)
     prob, sdf = fu.write_problem(p, str(tmp_path))
     exe = fu.build_driver(str(tmp_path))
     res, inp = str(tmp_path / "out.txt"), str(tmp_path / "in.txt")
     with open(inp, "w") as f:
-        f.write("7\n")
+        f.write(f"{kr} {flip}\n")
     r = subprocess.run([exe, prob, sdf, "pi_setnum", res, inp], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
     toks = open(res).read().split()
-    q = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=7)
+    q = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=kr,
+                        use_cumulative_costs=bool(flip) != p.params.use_cumulative_costs)
     q.sdf = p.sdf
     o = po.Oracle(q)
     K, pos = 12, 0
@@ -224,7 +231,7 @@ def test_facade_set_num_rollouts_moves_to_host(tmp_path):
         pos += 3
         oc, ocf = o.iterate(it)
         assert (cost, cf) == (oc, ocf), it
-        assert ngen == (K if it == 1 else K - 7)
+        assert ngen == (K if it == 1 else K - kr)
         th = np.array([float(x) for x in toks[pos:pos + p.J * p.N]]).reshape(p.J, p.N)
         pos += p.J * p.N
         np.testing.assert_array_equal(th, o.theta(), err_msg=f"theta it {it}")
