@@ -93,13 +93,14 @@ def workload_name(args) -> str:
     return args.workload + (" (modified)" if args.custom else "")
 
 
-def pmc_summary():
-    """The newest committed rocprofv3 PMC summary (tools/pmc_traffic.py) of the default workload
-    and whether it was taken of this build (the engine's source hash).  Returns (summary or None,
-    provenance dict)."""
+def pmc_summary(workload: str = "cfg2"):
+    """The newest committed rocprofv3 PMC summary (tools/pmc_traffic.py) of this workload on one
+    GPU and whether it was taken of this build (the engine's source hash).  Returns (summary or
+    None, provenance dict)."""
     from stomp_motion_planner_icra2011_amd import _build
     here = _build.source_hash()
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*rollout_cost_traffic*.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*rollout_cost_traffic*.json"), recursive=True),
+                   key=os.path.getmtime)
     newest = None
     for path in reversed(files):
         try:
@@ -107,13 +108,28 @@ def pmc_summary():
                 d = json.load(f)
         except Exception:
             continue
+        if d.get("workload", "cfg2") != workload:
+            continue
+        rel = os.path.relpath(path, os.path.join(ROOT, "profiles"))
         if newest is None:
-            newest = (os.path.basename(path), d.get("source_hash"))
+            newest = (rel, d.get("source_hash"))
         if d.get("source_hash") == here:
-            return d, {"file": os.path.basename(path), "source_hash": here, "matches_build": True}
-    return None, {"file": newest[0] if newest else None, "source_hash": newest[1] if newest else None,
-                  "build_source_hash": here, "matches_build": False,
-                  "note": "no PMC pass of this build is committed: traffic and VALU counts are null"}
+            return d, {"file": rel, "workload": workload, "source_hash": here, "matches_build": True}
+    return None, {"file": newest[0] if newest else None, "workload": workload,
+                  "source_hash": newest[1] if newest else None, "build_source_hash": here, "matches_build": False,
+                  "note": "no PMC pass of this build and workload is committed: traffic and VALU counts are null"}
+
+
+def pmc_fields(pmc, prov, avg_s):
+    """traffic (HBM bytes per launch of the dominant kernel) and its VALU issue, from a PMC summary"""
+    insts = pmc.get("valu_insts_per_launch") if pmc else None
+    return {"traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "traffic_uncorrected": pmc.get("hbm_bytes_per_launch_uncorrected") if pmc else None,
+            "traffic_source": prov,
+            "valu": {"insts_per_launch": insts,
+                     "issue_cycles_per_simd": round(insts * 4.0 / 1024, 1) if insts else None,
+                     "frac_valu_issue": round(insts * 4.0 / 1024 / (avg_s * VALU_CLOCK_HZ), 4) if insts else None,
+                     "clock_ghz": VALU_CLOCK_HZ / 1e9, "simds": 1024, "source": prov}}
 
 
 def cpu_share():
@@ -247,7 +263,7 @@ def bench_problems(args, world, rank, local_rank, dist):
         p = pb.make_problem(dof=args.dof, waypoints=args.waypoints, grid_n=args.grid,
                             num_rollouts=args.rollouts, num_reused_rollouts=0, build_grid=False,
                             seed=base.seed + 1 + i, start=list(base.start + d[0]), goal=list(base.goal + d[1]),
-                            max_iterations=args.warmup + args.steps + 1)
+                            max_iterations=args.warmup + 2 * args.steps + 1)
         k = i - first_id
         engines.append(eng.Engine(p, device=local_rank, sdf_device_ptr=sdf.ptr,
                                   stream=streams[k // gsize].ptr if gsize else None))
@@ -295,6 +311,39 @@ def bench_problems(args, world, rank, local_rank, dist):
         dist.barrier()
     elapsed = max_over_ranks(dist, elapsed)
     value = P_all * args.steps / elapsed
+
+    # the roofline of the dominant kernel, the grouped rollout launch (every engine of a group:
+    # k_rollout_group), timed with HIP events on the group's stream in a second pass of the same
+    # steps (stomp_group_run records its launches on its first engine's timers)
+    roofline = None
+    timing = {}
+    if groups and not args.no_timing:
+        e0 = groups[0].engines[0]
+        e0.set_timing(True)
+        sweep(args.warmup + args.steps + 1, args.steps)
+        for name in ("rollout_cost", "weights", "update"):
+            tot, n = e0.timing(name)
+            timing[name] = 1000.0 * tot / max(n, 1)
+        e0.set_timing(False)
+        S = len(base.spheres)
+        unit_bytes = 4 * S + 16 * base.J + 8
+        per_launch = len(groups[0].engines) * (args.rollouts + 1) * base.N   # (rollout, waypoint) units
+        avg_s = timing["rollout_cost"] * 1e-6
+        achieved = per_launch * unit_bytes / avg_s / 1e9
+        pmc, prov = pmc_summary("cfg5") if (world == 1 and not args.custom) else \
+            (None, {"note": "PMC summaries are of the BASELINE workloads on one GPU"})
+        pf = pmc_fields(pmc, prov, avg_s)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pf["traffic"],
+                    "traffic_uncorrected": pf["traffic_uncorrected"], "traffic_source": prov,
+                    "kernel": "k_rollout_group", "unit_bytes": unit_bytes, "units_per_launch": per_launch,
+                    "bytes_per_launch": per_launch * unit_bytes, "avg_launch_us": round(timing["rollout_cost"], 3),
+                    "sdf_only_gbs": round(per_launch * 4 * S / avg_s / 1e9, 2),
+                    "unit_bytes_actual": 2 * S + 16 * base.J + 8,
+                    "iteration_bytes": P_all * (args.rollouts + 1) * base.N * unit_bytes,
+                    "iteration_frac": round(P_all * (args.rollouts + 1) * base.N * unit_bytes * value / P_all /
+                                            (HBM_PEAK_GBS * 1e9 * world), 5),
+                    "valu": pf["valu"]}
     if rank == 0:
         print(json.dumps({
             "metric": "STOMP problem-iterations/sec (64-problem batch, cfg5)", "value": round(value, 3),
@@ -308,7 +357,9 @@ def bench_problems(args, world, rank, local_rank, dist):
                        "problems": P_all, "parallelism": f"replicas x{world}, " + (f"groups of {gsize} problems (shared launches)" if gsize else "one stream per problem"),
                        "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                        "enqueue_threads": threads, "group": gsize,
-                       "rollouts_per_s": round(value * args.rollouts, 1)}}))
+                       "rollouts_per_s": round(value * args.rollouts, 1)},
+            "roofline": roofline,
+            "kernel_timing_us": {k: round(v, 3) for k, v in timing.items()}}))
     for g in groups:
         g.close()
     for e in engines:
@@ -410,11 +461,13 @@ def main():
         avg_s = timing["rollout_cost"]["avg_us"] * 1e-6
         achieved = bytes_per_launch / avg_s / 1e9
         headline = args.workload == "cfg2" and not args.custom and world == 1
-        pmc, prov = pmc_summary() if headline else (None, {"note": "PMC summaries are of cfg2 on one GPU"})
+        one_gpu = not args.custom and world == 1
+        pmc, prov = pmc_summary(args.workload) if one_gpu else \
+            (None, {"note": "PMC summaries are of the BASELINE workloads on one GPU"})
+        pf = pmc_fields(pmc, prov, avg_s)
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5),
-                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-                    "traffic_uncorrected": pmc.get("hbm_bytes_per_launch_uncorrected") if pmc else None,
+                    "traffic": pf["traffic"], "traffic_uncorrected": pf["traffic_uncorrected"],
                     "traffic_source": prov,
                     "kernel": "k_rollout", "unit_bytes": unit_bytes, "units_per_launch": rows_launch * p.N,
                     "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(timing["rollout_cost"]["avg_us"], 3),
@@ -429,12 +482,7 @@ def main():
                     "iteration_frac": round((K - args.reused + 1) * p.N * unit_bytes * value /
                                             (HBM_PEAK_GBS * 1e9 * world), 5)}
         # the bound that actually binds: fp64 VALU issue (SQ_INSTS_VALU of the same build's PMC pass)
-        insts = pmc.get("valu_insts_per_launch") if pmc else None
-        roofline["valu"] = {
-            "insts_per_launch": insts,
-            "issue_cycles_per_simd": round(insts * 4.0 / 1024, 1) if insts else None,
-            "frac_valu_issue": round(insts * 4.0 / 1024 / (avg_s * VALU_CLOCK_HZ), 4) if insts else None,
-            "clock_ghz": VALU_CLOCK_HZ / 1e9, "simds": 1024, "source": prov}
+        roofline["valu"] = pf["valu"]
 
     # StompOptimizer::optimize (stomp_optimizer.cpp:249-401) through the device-resident loop:
     # the same iterations with the optimizer's bookkeeping, no early stop

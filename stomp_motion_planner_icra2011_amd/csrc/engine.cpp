@@ -2669,9 +2669,19 @@ int stomp_group_run(stomp_group* g, int32_t first, int32_t count)
     const int J = e0->J, N = e0->N, K = e0->K_loc;
     for (int i = 0; i < count; ++i) {
         unsigned char* base = g->d_args + per * i;
-        launch_cost_group(e0->model, g->d_models, (const CostArgs*)base, P, nro[i], K, s);
-        launch_weights_group((const WeightArgs*)(base + szc), P, J, N, K, s);
-        launch_update_group(J, N, (const UpdateArgs*)(base + szc + szw), P, s);
+        // with timing on for the group's first engine, its timers hold the group's launches
+        {
+            Timed tm(e0, T_COST, s);
+            launch_cost_group(e0->model, g->d_models, (const CostArgs*)base, P, nro[i], K, s);
+        }
+        {
+            Timed tm(e0, T_WEIGHTS, s);
+            launch_weights_group((const WeightArgs*)(base + szc), P, J, N, K, s);
+        }
+        {
+            Timed tm(e0, T_UPDATE, s);
+            launch_update_group(J, N, (const UpdateArgs*)(base + szc + szw), P, s);
+        }
     }
     err = hipGetLastError();
     if (err != hipSuccess) return gfail(g, STOMP_E_DEVICE, hipGetErrorString(err));

@@ -448,9 +448,10 @@ int weights_tile(int K_loc)
     return tc;
 }
 
-// Row tiles of four flat columns.  K_loc <= 1024: 512-lane workgroups (four or eight rows per
-// lane: the exp / division phases are per-lane chains, so more lanes finish them sooner; 12.5 ->
-// 11.5 us at cfg2 against 256 lanes); larger K_loc: 256 lanes with up to 32 rows per lane, and
+// Row tiles of four flat columns.  K_loc in (256, 1024]: 512-lane workgroups (four or eight rows
+// per lane: the exp / division phases are per-lane chains, so more lanes finish them sooner; 12.5
+// -> 11.5 us at cfg2 against 256 lanes); up to 256 rows 256 lanes (cfg1's 20 rows: 8.5 us against
+// 10.8 with 512); larger K_loc: 256 lanes with up to 32 rows per lane, and
 // for K_loc in (2048, 4096] two flat columns per workgroup so a lane's 32 rows still fit its
 // registers (the whole K = 4096 of cfg3 on one device; the one-column k_weights tiles read a
 // separate line per row there).  0 columns: the shape fits no row tile.
@@ -476,6 +477,7 @@ void launch_weights(const WeightArgs& a, hipStream_t s)
     const int K = a.K_loc;
     switch (rows_tcw(K)) {
     case 4:
+        if (K <= 4 * 64) return launch_rows_t<256, 4, 4>(a, s);   // few rows: the wider tile only waits longer
         if (K <= 4 * 128) return launch_rows_t<512, 4, 4>(a, s);
         if (K <= 8 * 128) return launch_rows_t<512, 4, 8>(a, s);
         if (K <= 16 * 64) return launch_rows_t<256, 4, 16>(a, s);
@@ -663,6 +665,7 @@ void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K
 {
     const int nt = weights_group_tiles(J, N, K_loc);
     if (nt <= 0 || engines <= 0) return;
+    if (K_loc <= 4 * 64) return launch_rows_group_t<256, 4>(as, engines, nt, K_loc, s);
     if (K_loc <= 4 * 128) return launch_rows_group_t<512, 4>(as, engines, nt, K_loc, s);
     if (K_loc <= 8 * 128) return launch_rows_group_t<512, 8>(as, engines, nt, K_loc, s);
     if (K_loc <= 16 * 64) return launch_rows_group_t<256, 16>(as, engines, nt, K_loc, s);

@@ -71,7 +71,7 @@ prof)
   tag=$1; shift
   mkdir -p gpurun_out/$tag
   [ $# -eq 0 ] && set -- --steps 200 --warmup 20
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 bench.py --cpu-seconds 0 "$@" > gpurun_out/$tag/bench.json 2> gpurun_out/$tag/bench.err || { tail -30 gpurun_out/$tag/bench.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 bench.py --cpu-seconds 0 --optimize-steps 0 "$@" > gpurun_out/$tag/bench.json 2> gpurun_out/$tag/bench.err || { tail -30 gpurun_out/$tag/bench.err; exit 1; }
   find gpurun_out/$tag -name "*kernel_stats.csv" | head -1 | xargs cat | cut -d, -f1-8 | head -20 ;;
 pmc)
   tag=$1; shift
@@ -89,7 +89,9 @@ art)
   bash tools/gpu.sh pmc art_${r}_pmc "$@" || exit 1
   mkdir -p gpurun_out/art_$r
   cp "$(find gpurun_out/art_${r}_prof -name '*kernel_stats.csv' | head -1)" gpurun_out/art_$r/kernel_stats.csv
-  python3 tools/pmc_traffic.py gpurun_out/art_${r}_pmc gpurun_out/art_$r/traffic.json gpurun_out/art_$r/kernel_stats.csv || exit 1
+  wl=cfg2; prev=""
+  for a in "$@"; do [ "$prev" = "--workload" ] && wl=$a; prev=$a; done
+  python3 tools/pmc_traffic.py gpurun_out/art_${r}_pmc gpurun_out/art_$r/traffic.json gpurun_out/art_$r/kernel_stats.csv $wl || exit 1
   bench_to gpurun_out/art_$r/bench.json 500 --cpu-seconds 0 "$@" || exit 1
   cat gpurun_out/art_$r/bench.json ;;
 final)

@@ -15,7 +15,9 @@ fraction: SQ_INSTS_VALU x 4 cycles (a wave64 instruction on a 16-lane SIMD) / (C
 The summary records the engine's source hash (_build.source_hash): bench.py reports these
 numbers only while the sources are the ones profiled.
 
-Usage: python tools/pmc_traffic.py <pmc dir> <out.json> [kernel_stats.csv]
+Usage: python tools/pmc_traffic.py <pmc dir> <out.json> [kernel_stats.csv [workload]]
+(workload: the bench.py --workload the passes ran, cfg2 by default; bench.py reports a summary for
+the workload it runs only)
 """
 import csv
 import collections
@@ -66,13 +68,15 @@ def main():
             e["avg_ns"] = durations[k]
             e["valu_issue_frac"] = round(d["SQ_INSTS_VALU"] * 4.0 / (256 * 4) / (durations[k] * 1e-9 * 2.4e9), 4)
         kernels[k] = e
+    workload = sys.argv[4] if len(sys.argv) > 4 else "cfg2"
     # the iteration's rollout launch: the k_rollout instantiation with the most dispatches (the
     # deferred noiseless flush at the end of a run is a different, rare launch)
     ro = [k for k in kernels if k.startswith("stomp::k_rollout")]
     stage = [max(ro, key=lambda k: kernels[k].get("dispatches", 0))] if ro else []
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE TCC_HIT_sum TCC_MISS_sum | SQ_* (separate passes), "
-                  "bench.py --steps 40 --warmup 5 --no-timing; per-dispatch means",
+                  "bench.py --workload " + workload + " --no-timing (tools/gpu.sh pmc); per-dispatch means",
+        "workload": workload,
         "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B, MI355X_MICROARCH.md:298, calibrated "
                       "for wide coalesced reads); the SDF gathers are 4-B lane loads, for which the factor is "
                       "uncalibrated, so the uncorrected figure (x1) is reported beside it: the true bytes lie "
