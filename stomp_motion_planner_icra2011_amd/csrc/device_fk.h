@@ -25,6 +25,36 @@ __device__ __forceinline__ void rotmul(const double* A, const double* B, double*
             C[3 * i + j] = A[3 * i + 0] * B[0 + j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
 }
 
+// the pose rotation rot * Rot2(axis, q) of a joint segment (q_index >= 0), (st, ct) = (sin q, cos q)
+__device__ __forceinline__ void pose_rotation(const DevSegment& sg, double st, double ct, double* R)
+{
+    const double* a = sg.axis;
+    const double vt = 1.0 - ct;
+    const double m_vt_0 = vt * a[0], m_vt_1 = vt * a[1], m_vt_2 = vt * a[2];
+    const double m_st_0 = a[0] * st, m_st_1 = a[1] * st, m_st_2 = a[2] * st;
+    const double m_vt_0_1 = m_vt_0 * a[1], m_vt_0_2 = m_vt_0 * a[2], m_vt_1_2 = m_vt_1 * a[2];
+    double Rq[9];
+    Rq[0] = ct + m_vt_0 * a[0];
+    Rq[1] = -m_st_2 + m_vt_0_1;
+    Rq[2] = m_st_1 + m_vt_0_2;
+    Rq[3] = m_st_2 + m_vt_0_1;
+    Rq[4] = ct + m_vt_1 * a[1];
+    Rq[5] = -m_st_0 + m_vt_1_2;
+    Rq[6] = -m_st_1 + m_vt_0_2;
+    Rq[7] = m_st_0 + m_vt_1_2;
+    Rq[8] = ct + m_vt_2 * a[2];
+    if (sg.rot_identity) {   // rot * Rq with rot = 1 is Rq (up to the sign of zeros; the oracle skips it too)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = Rq[k];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                R[3 * i + j] = sg.rot[3 * i + 0] * Rq[0 + j] + sg.rot[3 * i + 1] * Rq[3 + j] + sg.rot[3 * i + 2] * Rq[6 + j];
+    }
+}
+
 // out = parent * Frame(rot, trans) * Frame(Rot2(axis, q), 0), with (st, ct) = (sin q, cos q)
 // precomputed; parent == nullptr is the identity (root segment).  out must not alias parent.
 __device__ __forceinline__ void compose(const DevSegment& sg, const Frame* parent, double st, double ct, Frame& out)

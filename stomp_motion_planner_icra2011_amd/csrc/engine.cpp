@@ -138,6 +138,8 @@ struct stomp_engine {
     // sharded reuse (world > 1, K_r > 0): per-rank totals, all totals, the extra's total, the
     // chosen rows' slots [Kr][J N + N] and their all-gather [world][Kr][J N + N], the ranking
     double *d_tot_loc = nullptr, *d_tot_all = nullptr, *d_tot_x = nullptr, *d_slot = nullptr, *d_slot_all = nullptr;
+    double* d_reuse_costs = nullptr;   // one device: k_reuse's totals [K + 1] and its counter
+    int* d_reuse_count = nullptr;
     int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
     uint16_t* d_sdf = nullptr;   // d2 per voxel
@@ -653,7 +655,7 @@ int run_reuse(stomp_engine* e)
     if (e->world == 1) {
         if (int rc = launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, with_extra, e->d_params_b, e->d_state_b, e->d_control_b,
                          e->d_params, e->d_noise, e->d_state, e->d_x_params, e->d_x_state, e->d_x_control, e->d_theta,
-                         e->d_stop, e->stream))
+                         e->d_reuse_costs, e->d_reuse_count, e->d_stop, e->stream))
             return fail(e, STOMP_E_INVALID, rc == -1 ? "reuse: the source and destination rollout rows alias"
                                                      : "reuse: the cost rows of one candidate exceed the LDS");
         return 0;
@@ -1113,6 +1115,10 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     if (hipMemsetAsync(e->d_cs, 1, 1, e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "memset failed"));
     CREATE_TRY(dev_alloc(e, &e->d_pad_cf, 1));
+    if (e->world == 1 && e->Kr > 0) {   // k_reuse's per-candidate totals and its counter (zeroed)
+        CREATE_TRY(dev_alloc(e, &e->d_reuse_costs, (size_t)e->K + 1));
+        CREATE_TRY(dev_alloc(e, &e->d_reuse_count, 1));
+    }
     if (e->world > 1 && e->Kr > 0) {
         const size_t slot = (size_t)e->Kr * ((size_t)J * N + N);
         CREATE_TRY(dev_alloc(e, &e->d_tot_loc, (size_t)e->K_loc));
@@ -1299,6 +1305,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
     m.QT = e->d_QT;
+    // piece counters of the waypoint-split rollout launches (zeroed; the last piece resets its own)
+    CREATE_TRY(dev_alloc(e, &m.split_cnt, (size_t)e->K_loc + 2));
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
     int pad_cf = 0;

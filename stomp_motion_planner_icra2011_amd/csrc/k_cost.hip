@@ -21,6 +21,9 @@
 //   3. costs(t) = w_obs * state (:1148-1151), the collision flag and the total (:1155).
 // The extra workgroup (index num_noisy) evaluates the noiseless rollout of theta that the
 // previous iteration deferred (policy_improvement_loop.cpp:180-182).
+#include <algorithm>
+#include <cstdlib>
+
 #include "device_fk.h"
 #include "noise_device.h"
 #include "stamps.h"
@@ -45,6 +48,12 @@ constexpr int kBlock = ROLLOUT_BLOCK;
 #define ROLLOUT_WIDE_BLOCK 512
 #endif
 constexpr int kWideBlock = ROLLOUT_WIDE_BLOCK;
+// the waypoint-split rollout: workgroup size, most pieces per rollout
+#ifndef ROLLOUT_SPLIT_BLOCK
+#define ROLLOUT_SPLIT_BLOCK 512
+#endif
+constexpr int kSplitBlock = ROLLOUT_SPLIT_BLOCK;
+constexpr int kSplitMaxDefault = 4;
 template <int BLOCK>
 constexpr int rollout_min_waves()
 {
@@ -109,6 +118,147 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x)
     return max(max(a, b), max(c, d));
 }
 
+// handleJointLimits (stomp_optimizer.cpp:562-616) of the row in traj [J][N] (LDS) by the NW waves
+// of a workgroup; the caller publishes traj before and synchronises after.
+// Joints are independent: the limited joints are dealt round-robin over the waves and a wave
+// runs the passes of two of its joints in lockstep (pass p of one beside pass p of the other,
+// each joint still stopping on its own), so the two Q^-1 column loads of a step are in flight
+// together.  The argmax is a wave butterfly (every lane ends with the same (max, first
+// index)) and a pass needs no block barrier: LDS accesses of one wave execute in program order.
+// A joint without violations costs its wave one argmax.
+template <int NW>
+__device__ __forceinline__ void joint_limit_passes(const DevModel& m, double* traj, const int* hl_s,
+                                                   const double* jlim_s, int lane, int wv)
+{
+    const int J = m.J, N = m.N;
+    // A wave keeps its joints' rows in registers through the passes (lane l: waypoints l,
+    // l + 64, ...; N <= 256), so a pass is the argmax, the column load and the update with
+    // no LDS round trip; the rows go back to traj after the last pass.
+    // the violated waypoint a pass corrects (wave-uniform), -1 when none is left
+    auto jl_argmax = [&](const double* v, double jmin, double jmax) -> int {
+        double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
+        int ci = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = lane + 64 * u;
+            if (t < N) {
+                const double x = v[u];
+                double absamt = 0.0;
+                if (x > jmax) absamt = fabs(jmax - x);
+                else if (x < jmin) absamt = fabs(jmin - x);
+                if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
+            }
+        }
+        // wave argmax, first index on ties: the bits of a non-negative double order like
+        // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
+        const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
+        const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
+        const unsigned mh = wave_max_u32(hi);
+        const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
+        if ((mh | ml) == 0u) return -1;   // no violation left (wave-uniform)
+        const bool match = hi == mh && lo == ml;
+        int cm = 0;
+        for (int blk = 0; blk * 64 < N; ++blk) {
+            const unsigned long long b = __ballot(match && (ci >> 6) == blk);
+            if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
+        }
+        return cm;
+    };
+    // row += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
+    auto jl_apply = [&](double* v, int cm, double jmin, double jmax, const double* qv, double qd) {
+        double vu = v[0];
+#pragma unroll
+        for (int u = 1; u < 4; ++u)
+            if ((cm >> 6) == u) vu = v[u];   // uniform select
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
+        const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
+        const unsigned vhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), cm & 63);
+        const double x = __longlong_as_double((long long)(((unsigned long long)vhi << 32) | vlo));
+        const double amount = x > jmax ? jmax - x : jmin - x;
+        const double mult = amount / qd;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (lane + 64 * u < N) v[u] += mult * qv[u];
+    };
+    auto jl_pair = [&](int ja, int jb) {
+        const bool hb = jb >= 0;
+        const int jb0 = hb ? jb : ja;
+        const double amin = jlim_s[2 * ja], amax = jlim_s[2 * ja + 1];
+        const double bmin = jlim_s[2 * jb0], bmax = jlim_s[2 * jb0 + 1];
+        double va[4], vb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = min(lane + 64 * u, N - 1);
+            va[u] = traj[ja * N + t];
+            vb[u] = traj[jb0 * N + t];
+        }
+        bool la = true, lb = hb;
+        for (int pass = 0; pass < 11 && (la || lb); ++pass) {
+            int ca = -1, cb = -1;
+            if (la) { ca = jl_argmax(va, amin, amax); la = ca >= 0; }
+            if (lb) { cb = jl_argmax(vb, bmin, bmax); lb = cb >= 0; }
+            if (!la && !lb) break;
+            // both columns and diagonals in flight (unconditional loads, clamped; N <= 256)
+            const double* Qa = m.QT + ((size_t)ja * N + (size_t)max(ca, 0)) * N;
+            const double* Qb = m.QT + ((size_t)jb0 * N + (size_t)max(cb, 0)) * N;
+            double qa[4], qb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                qa[u] = Qa[min(lane + 64 * u, N - 1)];
+                qb[u] = Qb[min(lane + 64 * u, N - 1)];
+            }
+            const double qda = Qa[max(ca, 0)], qdb = Qb[max(cb, 0)];
+            if (la) jl_apply(va, ca, amin, amax, qa, qda);
+            if (lb) jl_apply(vb, cb, bmin, bmax, qb, qdb);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = lane + 64 * u;
+            if (t < N) {
+                traj[ja * N + t] = va[u];
+                if (hb) traj[jb * N + t] = vb[u];
+            }
+        }
+    };
+    int mine = -1, k = 0;
+    for (int j = 0; j < J; ++j) {
+        if (!hl_s[j]) continue;
+        if (k++ % NW != wv) continue;
+        if (mine < 0) {
+            mine = j;
+        } else {
+            jl_pair(mine, j);
+            mine = -1;
+        }
+    }
+    if (mine >= 0) jl_pair(mine, -1);
+}
+
+// a rollout launch's block past its rollouts: pregen row r of the next iteration (normals,
+// sigma L z, M eps), left at the default wave priority while the rollout waves raise theirs, so
+// it takes the issue slots the latency-bound rollout waves leave idle and the CUs the
+// early-finishing rollouts free; no stop check (the rows stay valid for pre_it).  First, unless
+// its rollout prices it (own), this iteration's row r (ctl_by_pre).  pA / pB: LDS buffers of the
+// noise phase
+template <int BLOCK>
+__device__ __forceinline__ void pregen_block(const CostArgs& a, int r, bool own, double* pA, double* pB)
+{
+    const NoiseArgs& pa = a.pre_next;
+    if (a.ctl_by_pre && r < a.ctl_rows && !own && !(a.stop && *a.stop)) {
+        // this iteration's row r priced here instead of on its rollout's critical path
+        pre_row_control<BLOCK>(a.nz, r, pA, pB, threadIdx.x);
+        __syncthreads();   // pA / pB are the normals' buffers next
+    }
+    rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
+    if (pa.J <= 8) {
+        pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
+        pregen_meps_ng<BLOCK, 2>(pa, r, pB, threadIdx.x);
+    } else {
+        pregen_eps_ng<BLOCK, 4>(pa, r, pA, pB, threadIdx.x);
+        pregen_meps_ng<BLOCK, 4>(pa, r, pB, threadIdx.x);
+    }
+}
+
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
 // FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
@@ -130,25 +280,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // the early-finishing rollouts free; no stop check (the rows stay valid for pre_it)
         const int nro = a.num_noisy + (a.x_params ? 1 : 0);
         if (bid >= nro) {
-            const NoiseArgs& pa = a.pre_next;
-            double* pA = (double*)(lds_raw + L.nzA);
-            double* pB = (double*)(lds_raw + L.nzB);
             const int r = bid - nro;
             // a phased launch's rollouts price their own rows (the FK-idle waves)
             const bool own = PHASED && r >= a.row0 && r < a.row0 + a.num_noisy;
-            if (a.ctl_by_pre && r < a.ctl_rows && !own && !(a.stop && *a.stop)) {
-                // this iteration's row r priced here instead of on its rollout's critical path
-                pre_row_control<BLOCK>(a.nz, r, pA, pB, threadIdx.x);
-                __syncthreads();   // pA / pB are the normals' buffers next
-            }
-            rollout_normals<BLOCK>(pa, r, pA, pB, threadIdx.x);
-            if (J <= 8) {
-                pregen_eps_ng<BLOCK, 2>(pa, r, pA, pB, threadIdx.x);
-                pregen_meps_ng<BLOCK, 2>(pa, r, pB, threadIdx.x);
-            } else {
-                pregen_eps_ng<BLOCK, 4>(pa, r, pA, pB, threadIdx.x);
-                pregen_meps_ng<BLOCK, 4>(pa, r, pB, threadIdx.x);
-            }
+            pregen_block<BLOCK>(a, r, own, (double*)(lds_raw + L.nzA), (double*)(lds_raw + L.nzB));
             return;
         }
     }
@@ -245,117 +380,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     STAMP(1);
     BLOCK_MARK(4);
 
-    // ---- handleJointLimits
-    // Joints are independent: the limited joints are dealt round-robin over the waves and a wave
-    // runs the passes of two of its joints in lockstep (pass p of one beside pass p of the other,
-    // each joint still stopping on its own), so the two Q^-1 column loads of a step are in flight
-    // together.  The argmax is a wave butterfly (every lane ends with the same (max, first
-    // index)) and a pass needs no block barrier: LDS accesses of one wave execute in program order.
-    // A joint without violations costs its wave one argmax (no block-wide pre-scan: the barrier
-    // above already published traj).
+    // ---- handleJointLimits (no block-wide pre-scan: the barrier above already published traj)
     {
         __builtin_amdgcn_s_setprio(3);   // a dependent chain per joint (critical path)
-        // A wave keeps its joints' rows in registers through the passes (lane l: waypoints l,
-        // l + 64, ...; N <= 256), so a pass is the argmax, the column load and the update with
-        // no LDS round trip; the rows go back to traj after the last pass.
-        // the violated waypoint a pass corrects (wave-uniform), -1 when none is left
-        auto jl_argmax = [&](const double* v, double jmin, double jmax) -> int {
-            double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
-            int ci = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = lane + 64 * u;
-                if (t < N) {
-                    const double x = v[u];
-                    double absamt = 0.0;
-                    if (x > jmax) absamt = fabs(jmax - x);
-                    else if (x < jmin) absamt = fabs(jmin - x);
-                    if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
-                }
-            }
-            // wave argmax, first index on ties: the bits of a non-negative double order like
-            // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
-            const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
-            const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
-            const unsigned mh = wave_max_u32(hi);
-            const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
-            if ((mh | ml) == 0u) return -1;   // no violation left (wave-uniform)
-            const bool match = hi == mh && lo == ml;
-            int cm = 0;
-            for (int blk = 0; blk * 64 < N; ++blk) {
-                const unsigned long long b = __ballot(match && (ci >> 6) == blk);
-                if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
-            }
-            return cm;
-        };
-        // row += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
-        auto jl_apply = [&](double* v, int cm, double jmin, double jmax, const double* qv, double qd) {
-            double vu = v[0];
-#pragma unroll
-            for (int u = 1; u < 4; ++u)
-                if ((cm >> 6) == u) vu = v[u];   // uniform select
-            const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
-            const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
-            const unsigned vhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), cm & 63);
-            const double x = __longlong_as_double((long long)(((unsigned long long)vhi << 32) | vlo));
-            const double amount = x > jmax ? jmax - x : jmin - x;
-            const double mult = amount / qd;
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (lane + 64 * u < N) v[u] += mult * qv[u];
-        };
-        auto jl_pair = [&](int ja, int jb) {
-            const bool hb = jb >= 0;
-            const int jb0 = hb ? jb : ja;
-            const double amin = jlim_s[2 * ja], amax = jlim_s[2 * ja + 1];
-            const double bmin = jlim_s[2 * jb0], bmax = jlim_s[2 * jb0 + 1];
-            double va[4], vb[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = min(lane + 64 * u, N - 1);
-                va[u] = traj[ja * N + t];
-                vb[u] = traj[jb0 * N + t];
-            }
-            bool la = true, lb = hb;
-            for (int pass = 0; pass < 11 && (la || lb); ++pass) {
-                int ca = -1, cb = -1;
-                if (la) { ca = jl_argmax(va, amin, amax); la = ca >= 0; }
-                if (lb) { cb = jl_argmax(vb, bmin, bmax); lb = cb >= 0; }
-                if (!la && !lb) break;
-                // both columns and diagonals in flight (unconditional loads, clamped; N <= 256)
-                const double* Qa = m.QT + ((size_t)ja * N + (size_t)max(ca, 0)) * N;
-                const double* Qb = m.QT + ((size_t)jb0 * N + (size_t)max(cb, 0)) * N;
-                double qa[4], qb[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    qa[u] = Qa[min(lane + 64 * u, N - 1)];
-                    qb[u] = Qb[min(lane + 64 * u, N - 1)];
-                }
-                const double qda = Qa[max(ca, 0)], qdb = Qb[max(cb, 0)];
-                if (la) jl_apply(va, ca, amin, amax, qa, qda);
-                if (lb) jl_apply(vb, cb, bmin, bmax, qb, qdb);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = lane + 64 * u;
-                if (t < N) {
-                    traj[ja * N + t] = va[u];
-                    if (hb) traj[jb * N + t] = vb[u];
-                }
-            }
-        };
-        int mine = -1, k = 0;
-        for (int j = 0; j < J; ++j) {
-            if (!hl_s[j]) continue;
-            if (k++ % NW != wv) continue;
-            if (mine < 0) {
-                mine = j;
-            } else {
-                jl_pair(mine, j);
-                mine = -1;
-            }
-        }
-        if (mine >= 0) jl_pair(mine, -1);
+        joint_limit_passes<NW>(m, traj, hl_s, jlim_s, lane, wv);
         __builtin_amdgcn_s_setprio(2);
         __syncthreads();
     }
@@ -774,6 +802,446 @@ __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_g
     rollout_body<BLOCK, false, false>(ms[p], as[p], bid);
 }
 
+// ---- the waypoint-split rollout (k_rollout_split): when a launch's rollouts fit P >= 2 to a CU
+// (the K-sharded ranks, cfg1, the deferred noiseless rollout) rollout e runs on P workgroups,
+// piece p owning the free waypoints [t0, t1) = [p N / P, (p + 1) N / P).  Everything but the
+// joint-limit passes is per waypoint or needs a halo of the velocity stencil's taps
+// (stomp_optimizer.cpp:618-709, 1096-1105): each piece makes the whole row and runs
+// handleJointLimits on it (as the one-workgroup rollout does), then the FK program on the
+// waypoints [x0, x1) = [t0 - 1, t1 + 2) clamped to [0, N) (one lane per waypoint, every slot's
+// frame kept in LDS), the (sphere, waypoint) pairs of its own waypoints, their velocities and the
+// fold.  The last piece of a rollout to finish (a per-rollout counter, agent-scope release /
+// acquire, no waiting) reads the N costs back and makes costs.sum() (:1155) and the collision
+// flag.  Same expressions, same order per waypoint: bit-identical to the other bodies.
+namespace {
+constexpr int kSplitHaloL = 3 - kVelTap0;   // velocity taps reach t - 1 .. t + 2
+constexpr int kSplitHaloR = kVelTap1 - 3;
+}
+
+struct SplitLds {
+    size_t traj, ps, sv, fb, av, nzl, zA, zB, img, total;
+};
+
+// W: FK waypoints of the widest piece, Wo: its own waypoints
+__host__ __device__ inline SplitLds split_lds(int J, int N, int S, int nsaves, int nslots, int W, int Wo,
+                                              size_t img_bytes)
+{
+    SplitLds l;
+    l.traj = 0;
+    l.ps = l.traj + (size_t)J * N * sizeof(double);                // pose rotations [J][9][W]
+    l.sv = l.ps + (size_t)J * 9 * W * sizeof(double);              // saved frames [nsaves][12][W]
+    l.fb = l.sv + (size_t)nsaves * 12 * W * sizeof(double);        // slot frames [nslots][12][W]
+    l.av = l.fb + (size_t)nslots * 12 * W * sizeof(double);        // a values [S][Wo]
+    l.nzl = l.av + (size_t)S * Wo * sizeof(double);                // non-zero pairs
+    // the noise phase's buffers alias the pair buffers (dead until the pairs)
+    const size_t nzw = (size_t)(N + kBandBatch) * noise_jp(J) > (size_t)J * (N + 12)
+                           ? (size_t)(N + kBandBatch) * noise_jp(J) : (size_t)J * (N + 12);
+    l.zA = l.av;
+    l.zB = l.zA + nzw * sizeof(double);
+    size_t end = l.nzl + (size_t)S * Wo * sizeof(unsigned short);
+    if (l.zB + nzw * sizeof(double) > end) end = l.zB + nzw * sizeof(double);
+    l.img = align16(end);
+    l.total = l.img + img_bytes;
+    return l;
+}
+
+__host__ __device__ inline void split_range(int N, int P, int p, int& t0, int& t1, int& x0, int& x1)
+{
+    t0 = p * N / P;
+    t1 = (p + 1) * N / P;
+    x0 = t0 - kSplitHaloL < 0 ? 0 : t0 - kSplitHaloL;
+    x1 = t1 + kSplitHaloR > N ? N : t1 + kSplitHaloR;
+}
+
+// sphere_speed with the frames of waypoints [x0, x0 + W) in fb ([12][W])
+__device__ __forceinline__ double sphere_speed_w(const DevModel& m, const double* fb, int W, int x0,
+                                                 const double* pad, const DevSphere& sp, int s, int t)
+{
+    const int N = m.N;
+    double y[7][3];
+#pragma unroll
+    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
+        const int tt = t + kk - 3;
+        double yf[3];
+        apply_lds(fb, W, min(max(tt, 0), N - 1) - x0, sp.pos, yf);
+        const int row = tt < 0 ? tt + 6 : (tt >= N ? tt - N + 6 : 0);
+        const double* src = pad + (row * m.S + s) * 3;
+        const bool in = tt >= 0 && tt < N;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) y[kk][c] = in ? yf[c] : src[c];
+    }
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+#pragma unroll
+    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
+        const double c = m.vel_coef[kk];
+        if (c == 0.0) continue;
+        v0 += c * y[kk][0];
+        v1 += c * y[kk][1];
+        v2 += c * y[kk][2];
+    }
+    return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(DevModel m, CostArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    __shared__ int flag, nz_count, last;
+    const int J = m.J, N = m.N, S = m.S, P = a.split;
+    const int nro = a.num_noisy + (a.x_params ? 1 : 0);
+    const int Wmax = (N + P - 1) / P + kSplitHaloL + kSplitHaloR, Womax = (N + P - 1) / P;
+    const RolloutLds R = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
+    const int nw = (int)((R.pad - R.sph) / 8);   // the table image without the padding positions
+    const SplitLds L = split_lds(J, N, S, m.nsaves, m.nslots, Wmax, Womax, (size_t)nw * 8);
+    const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int NW = BLOCK / 64;
+    double* zA = (double*)(lds_raw + L.zA);
+    double* zB = (double*)(lds_raw + L.zB);
+    if (bid >= nro * P) {
+        pregen_block<BLOCK>(a, bid - nro * P, false, zA, zB);
+        return;
+    }
+    if (a.pre_rows > 0) __builtin_amdgcn_s_setprio(2);
+    if (a.stop && *a.stop) return;
+    STAMP(200);
+    BLOCK_BEGIN();
+    const int e = bid / P, piece = bid - e * P;
+    int t0, t1, x0, x1;
+    split_range(N, P, piece, t0, t1, x0, x1);
+    const int W = x1 - x0, Wo = t1 - t0;
+    // the table image's parts at their offsets relative to its start (RolloutLds from .sph); the
+    // padding-row positions (read by the velocities at the trajectory's ends only) stay in HBM
+    unsigned char* img0 = lds_raw + L.img - R.sph;
+    const DevSphere* sph = (const DevSphere*)(img0 + R.sph);
+    const DevSegment* seg_s = (const DevSegment*)(img0 + R.seg);
+    const FkOp* ops_s = (const FkOp*)(img0 + R.ops);
+    const int* hl_s = (const int*)(img0 + R.hl);
+    const double* jlim_s = (const double*)(img0 + R.jlim);
+    const double* pad = m.pad_pos;
+    double* traj = (double*)(lds_raw + L.traj);
+    double* ps = (double*)(lds_raw + L.ps);
+    double* sv = (double*)(lds_raw + L.sv);
+    double* fb = (double*)(lds_raw + L.fb);
+    double* av = (double*)(lds_raw + L.av);
+    unsigned short* nzl = (unsigned short*)(lds_raw + L.nzl);
+
+    // ---- the row (as rollout_body), the table image copied meanwhile
+    const bool extra = e == a.num_noisy;
+    const int member = extra ? a.x_member : a.member;
+    const bool gen = a.fused_noise == 1 && !extra;
+    const bool pre = a.fused_noise == 2 && !extra;
+    const bool priced = a.ctl_by_pre;
+    const int pr = e + a.row0;
+    constexpr int kCopyBatch = 12 * 256 / BLOCK;
+    unsigned long long img[kCopyBatch];
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
+    PreChunk pc0;
+    if (pre) {
+        if (priced) pre_chunk_load<BLOCK, false>(a.nz, pr, 0, tid, pc0);
+        else pre_chunk_load<BLOCK>(a.nz, pr, 0, tid, pc0);
+    }
+    // the row's noise / params / control stores: every piece computes the same values; the
+    // control rows are dealt over the pieces by joint (defer), the rest is stored by all
+    if (gen) {
+        rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
+    } else if (!pre) {
+        const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
+        const bool xc = extra && a.x_ctl && piece == 0;   // the extra rollout's rows (addExtraRollouts)
+        for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = prm[min(idx0 + tid + u * BLOCK, J * N - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int idx = idx0 + tid + u * BLOCK;
+                if (idx < J * N) {
+                    traj[idx] = v[u];
+                    if (xc) {
+                        a.x_prm[idx] = v[u];
+                        a.x_nse[idx] = 0.0;
+                        const int d = idx / N, i = idx - d * N;
+                        zA[d * m.Nall + i + 6] = v[u] + 0.0;
+                    }
+                }
+            }
+        }
+        if (xc) rollout_control<BLOCK>(a.nz, 0, zA, zB, tid, a.x_ctl);
+    }
+    {
+        unsigned long long* dst = (unsigned long long*)(lds_raw + L.img);
+#pragma unroll
+        for (int u = 0; u < kCopyBatch; ++u)
+            if (tid + u * BLOCK < nw) dst[tid + u * BLOCK] = img[u];
+        for (int w = tid + kCopyBatch * BLOCK; w < nw; w += BLOCK) dst[w] = m.img[w];
+    }
+    STAMP(201);
+    const bool defer = gen || (pre && !priced);
+    if (gen) rollout_project<BLOCK, true>(a.nz, e, traj, zA, zB, tid);
+    else if (pre) {
+        if (priced) rollout_from_pre<BLOCK, true, false>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
+        else rollout_from_pre<BLOCK, true>(a.nz, pr, e == 0, traj, zA, zB, tid, pc0);
+    }
+    if (tid == 0) { flag = 0; nz_count = 0; }
+    __syncthreads();
+    STAMP(202);
+    BLOCK_MARK(4);
+
+    // ---- handleJointLimits on the whole row (every piece: the passes couple the waypoints)
+    __builtin_amdgcn_s_setprio(3);
+    joint_limit_passes<NW>(m, traj, hl_s, jlim_s, lane, wv);
+    __builtin_amdgcn_s_setprio(2);
+    __syncthreads();
+    STAMP(203);
+    BLOCK_MARK(5);
+    double* tout = extra ? a.x_traj : (a.traj_out ? a.traj_out + (long long)e * J * N : nullptr);
+    if (tout)
+        for (int idx = tid; idx < J * Wo; idx += BLOCK) {
+            const int d = idx / Wo, t = t0 + idx - d * Wo;
+            tout[d * N + t] = traj[d * N + t];
+        }
+    // the joint segments' pose rotations at the piece's FK waypoints (rot * Rot2(axis, q), as
+    // compose makes them), one (segment, waypoint) per lane, into ps [q][9][W]
+    __syncthreads();
+    for (int idx = tid; idx < m.nseg * W; idx += BLOCK) {
+        const int g = idx / W, l = idx - g * W;
+        const DevSegment& sg = seg_s[g];
+        if (sg.q_index < 0) continue;
+        double st, ct, R[9];
+        det_sincos(traj[sg.q_index * N + x0 + l], &st, &ct);
+        pose_rotation(sg, st, ct, R);
+        double* dst = ps + (size_t)sg.q_index * 9 * W + l;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) dst[k * W] = R[k];
+    }
+    __syncthreads();
+    STAMP(204);
+
+    // ---- FK program, row-parallel: frame row r (R[r][0..2], p[r]) depends only on the parent's
+    // row r and the pose (compose's products, element by element), so wave fk0 + r runs row r of
+    // every frame (lane l: waypoint x0 + l) and writes it to the saved / slot frames; the other
+    // waves price the control rows this piece is dealt (joints piece, piece + P, ...)
+    const int fk0 = NW >= 8 ? ((bid & 1) ? 5 : 0) : (bid & 1);
+    const int r = wv - fk0;
+    if (r >= 0 && r < 3) {
+        __builtin_amdgcn_s_setprio(3);
+        if (lane < W) {
+            double c0 = 0.0, c1 = 0.0, c2 = 0.0, cp = 0.0;   // row r of the running frame
+            for (int op = 0; op < m.nops; ++op) {
+                const FkOp o = ops_s[op];
+                if (o.seg >= 0) {
+                    const DevSegment& sg = seg_s[o.seg];
+                    double PR[9];
+                    if (sg.q_index >= 0) {
+                        const double* src = ps + (size_t)sg.q_index * 9 * W + lane;
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) PR[k] = src[k * W];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) PR[k] = sg.rot[k];
+                    }
+                    double b0 = c0, b1 = c1, b2 = c2, bp = cp;
+                    if (o.base >= 0) {
+                        const double* src = sv + (size_t)o.base * 12 * W + lane;
+                        b0 = src[(3 * r + 0) * W];
+                        b1 = src[(3 * r + 1) * W];
+                        b2 = src[(3 * r + 2) * W];
+                        bp = src[(9 + r) * W];
+                    }
+                    if (o.base == kBaseRoot) {   // the pose itself (r is wave-uniform: selects, no indexing)
+                        c0 = r == 0 ? PR[0] : (r == 1 ? PR[3] : PR[6]);
+                        c1 = r == 0 ? PR[1] : (r == 1 ? PR[4] : PR[7]);
+                        c2 = r == 0 ? PR[2] : (r == 1 ? PR[5] : PR[8]);
+                        cp = sg.trans[r];
+                    } else {
+                        if (sg.q_index < 0 && sg.rot_identity) {   // parent * 1
+                            c0 = b0; c1 = b1; c2 = b2;
+                        } else {
+                            c0 = b0 * PR[0] + b1 * PR[3] + b2 * PR[6];
+                            c1 = b0 * PR[1] + b1 * PR[4] + b2 * PR[7];
+                            c2 = b0 * PR[2] + b1 * PR[5] + b2 * PR[8];
+                        }
+                        cp = b0 * sg.trans[0] + b1 * sg.trans[1] + b2 * sg.trans[2] + bp;
+                    }
+                    if (o.save >= 0) {
+                        double* dst = sv + (size_t)o.save * 12 * W + lane;
+                        dst[(3 * r + 0) * W] = c0;
+                        dst[(3 * r + 1) * W] = c1;
+                        dst[(3 * r + 2) * W] = c2;
+                        dst[(9 + r) * W] = cp;
+                    }
+                }
+                if (o.slot >= 0) {
+                    double* dst = fb + (size_t)o.slot * 12 * W + lane;
+                    dst[(3 * r + 0) * W] = c0;
+                    dst[(3 * r + 1) * W] = c1;
+                    dst[(3 * r + 2) * W] = c2;
+                    dst[(9 + r) * W] = cp;
+                }
+            }
+        }
+        __builtin_amdgcn_s_setprio(2);
+    } else if (defer) {
+        const int cw = wv < fk0 ? wv : wv - 3;
+        for (int d = piece + P * cw; d < J; d += P * (NW - 3))
+            wave_control(a.nz, (size_t)pr * J * N, zA, zB, d, lane);
+    }
+    __syncthreads();   // every slot's frame published (and the control rows' LDS use done)
+    STAMP(205);
+
+    // ---- pairs of the own waypoints: lane (g, tl) takes spheres [g CPL, (g + 1) CPL) at t0 + tl
+    bool col = false;
+    {
+        const int G = BLOCK / Wo, pg = tid / Wo, pt = tid - pg * Wo;
+        const int CPL = (S + G - 1) / G;
+        const int fc = t0 - x0 + pt;   // the lane's frame column
+        if (pg < G) {
+            double F[12];
+            int fslot = -1;
+            for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
+                unsigned dv[kLaneSpheres];
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    if (u0 + u >= CPL) break;   // uniform
+                    const int sc = min(pg * CPL + u0 + u, S - 1);
+                    const DevSphere& sp = sph[sc];
+                    if (sp.slot != fslot) {
+                        fslot = sp.slot;
+                        const double* src = fb + (size_t)fslot * 12 * W + fc;
+#pragma unroll
+                        for (int k = 0; k < 12; ++k) F[k] = src[k * W];
+                    }
+                    double x[3];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+                        x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
+                    dv[u] = sdf_d2(m, x);
+                }
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    if (u0 + u >= CPL) break;   // uniform
+                    const int sq = pg * CPL + u0 + u;
+                    bool nz = false;
+                    if (sq < S) {
+                        const DevSphere& sp = sph[sq];
+                        const int d2 = (int)dv[u];
+                        col |= d2 < sp.col_lim;
+                        nz = d2 < sp.zero_lim;
+                        av[sq * Wo + pt] = nz ? (double)d2 : 0.0;
+                    }
+                    const unsigned long long mask = __ballot(nz);
+                    if (mask) {
+                        const int leader = __ffsll((long long)mask) - 1;
+                        int base = 0;
+                        if (lane == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                        base = __shfl(base, leader, 64);
+                        if (nz) nzl[base + __popcll(mask & ((1ull << lane) - 1ull))] = (unsigned short)(sq * Wo + pt);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();   // pots and the non-zero list complete
+    STAMP(206);
+    __builtin_amdgcn_s_setprio(3);
+    for (int i = tid; i < nz_count; i += BLOCK) {
+        const int it = nzl[i];
+        const int qi = it / Wo, tl = it - qi * Wo;
+        const DevSphere& sp = sph[qi];
+        const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
+        av[it] = pot * sphere_speed_w(m, fb + (size_t)sp.slot * 12 * W, W, x0, pad, sp, qi, t0 + tl);
+    }
+    if (col) flag = 1;   // every writer stores 1
+    __syncthreads();   // every a value complete
+    STAMP(207);
+    double* so = extra ? a.x_state : a.state_out + (long long)e * N;
+    uint8_t* cfo = extra ? a.x_cf : (a.cf_out ? a.cf_out + e : nullptr);
+    double* to = extra ? a.x_total : (a.total_out ? a.total_out + e : nullptr);
+    const bool combine = cfo || to;   // workgroup-uniform
+    if (tid < Wo) {
+        // fold in sphere order
+        double cum = 0.0, state = 0.0;
+        for (int q0 = 0; q0 < S; q0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, S - 1) * Wo + tid];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                if (q0 + q >= S) break;
+                cum += v[q];
+                state += cum;
+            }
+        }
+        so[t0 + tid] = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
+        if (combine) __threadfence();   // release: the costs before this piece counts itself done
+    }
+    __builtin_amdgcn_s_setprio(2);
+    STAMP(208);
+    if (!combine) return;
+    __syncthreads();
+    BLOCK_END();
+    if (tid == 0) {
+        // pieces done in the low 16 bits, pieces that saw a collision above
+        const int add = 1 + (flag ? 1 << 16 : 0);
+        const int old = atomicAdd(a.split_cnt + e, add);
+        last = (old & 0xffff) == P - 1 ? 1 + ((old + add) >> 16 > 0 ? 2 : 0) : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();   // acquire: the other pieces' costs
+    if (to && tid < N) av[tid] = so[tid];
+    __syncthreads();
+    if (tid == 0) {
+        const bool any_col = (last & 2) != 0;
+        const bool cf = !any_col && !(member == 0 && m.pad_collision);
+        if (cfo) *cfo = cf ? 1 : 0;
+        if (to) {
+            // costs.sum() (:1155), sequential
+            double s = 0.0;
+            int k = 0;
+            for (; k + 8 <= N; k += 8) {
+                double v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = av[k + q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) s += v[q];
+            }
+            for (; k < N; ++k) s += av[k];
+            *to = s;
+        }
+        a.split_cnt[e] = 0;   // for the next launch (stream order)
+    }
+    STAMP(209);
+}
+
+// pieces per rollout of a launch of nro rollouts and pre_rows pregen blocks (0: the split body
+// does not apply)
+int split_pieces(const DevModel& m, int nro, int pre_rows)
+{
+    if (!m.split_cnt || nro <= 0) return 0;
+    // STOMP_DEBUG_SPLIT_MAX: most pieces per rollout (1: the phased body; tests and A/B)
+    const char* env = getenv("STOMP_DEBUG_SPLIT_MAX");
+    const int cap = env ? atoi(env) : kSplitMaxDefault;
+    int P = std::min(m.cus / nro, std::min(cap, m.N));
+    if (P < 2) return 0;
+    // the launch's pregen blocks share it: past two workgroups per CU the split pieces take the
+    // CUs those blocks need (a gather-mode rank's 65 rollouts beside 512 pregen rows: the phased
+    // one-workgroup body is faster there, 40.5 against 44.2 us)
+    if (nro * P + pre_rows > 2 * m.cus) return 0;
+    // one FK wave per piece
+    const int Pmin = (m.N + 63 - kSplitHaloL - kSplitHaloR - 1) / (64 - kSplitHaloL - kSplitHaloR);
+    if (P < Pmin) return 0;
+    if ((size_t)m.S * ((m.N + P - 1) / P) > 65535) return 0;   // pair ids are 16-bit
+    return P;
+}
+
+size_t rollout_split_lds_bytes(const DevModel& m, int P)
+{
+    const int Wo = (m.N + P - 1) / P, W = Wo + kSplitHaloL + kSplitHaloR;
+    const RolloutLds R = rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds);
+    return split_lds(m.J, m.N, m.S, m.nsaves, m.nslots, W, Wo, R.pad - R.sph).total;
+}
+
 STOMP_STAMP_ACCESSORS(cost)
 
 // generateRollouts' normals and eps = sigma L z, computeProjectedNoise's M eps for one row per
@@ -872,6 +1340,18 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     const int blocks = nro + (a.pre_rows > 0 ? a.pre_rows : 0);
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
+    if (const int P = split_pieces(m, nro, a.pre_rows > 0 ? a.pre_rows : 0)) {
+        const size_t ls = rollout_split_lds_bytes(m, P);
+        if (ls + 1024 <= kRolloutLdsMax) {
+            CostArgs b = a;
+            b.split = P;
+            b.split_cnt = m.split_cnt;
+            lds_opt_in((const void*)k_rollout_split<kSplitBlock>, ls);
+            hipLaunchKernelGGL((k_rollout_split<kSplitBlock>), dim3(nro * P + (a.pre_rows > 0 ? a.pre_rows : 0)),
+                               dim3(kSplitBlock), ls, s, m, b);
+            return;
+        }
+    }
     if (kWideBlock != kBlock && nro <= m.cus && m.phased_lds > 0) {
         const size_t lp = m.phased_lds;
         lds_opt_in((const void*)k_rollout_phased, lp);

@@ -155,56 +155,48 @@ __device__ __forceinline__ void reuse_totals_block(int c0, int c1, int K, int J,
 // K previous rollouts and the extra (noiseless) rollout by Rollout::getCost (:149-156),
 // lexicographic on (cost, index) with the extra rollout at index -1 (std::sort of pairs), copy
 // the best K_r into rows K_gen.. and re-base their noise on the current theta.
-// One 1024-lane workgroup, latency-bound throughout, so every phase puts all its loads in flight
-// at once: the candidates' cost rows (state row + J control rows, P = (J + 1) N doubles each) are
-// staged in LDS a chunk of candidates at a time with at most P / 1024 + 1 loads per lane per
-// candidate and nothing waiting between them; the J + 1 t-chains of each candidate then run out of
-// LDS (lane per chain, the order and roundings of chain_sum), the ranking, and the kept rows copied
-// with all their loads in flight.
+// One 1024-lane workgroup per candidate prices it: its cost rows (state row + J control rows,
+// (J + 1) N doubles) staged in LDS with every load in flight, the J + 1 t-chains out of LDS (lane
+// per chain, chain_sum's order and roundings), the total to costs_g; the last workgroup to finish
+// (a counter, agent-scope release / acquire, no waiting) ranks all candidates and copies the kept
+// rows with all their loads in flight.
 constexpr int kReuseBlock = 1024;
-constexpr size_t kReuseLds = 156 * 1024;   // the workgroup's LDS: staged cost rows + sums + totals
+constexpr size_t kReuseLds = 156 * 1024;
 
-// per: candidates staged per chunk (launch_reuse sizes it to the LDS)
-__global__ __launch_bounds__(kReuseBlock) void k_reuse(int per, int K, int J, int N, int Kr, int K_gen, int with_extra,
+__global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra,
                                                        const double* src_params, const double* src_state,
                                                        const double* control, double* params, double* noise,
                                                        double* state, const double* x_params, const double* x_state,
-                                                       const double* x_control, const double* theta, const int* stop)
+                                                       const double* x_control, const double* theta, double* costs_g,
+                                                       int* count, const int* stop)
 {
     if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
+    __shared__ double part[kMaxJoints + 1];
+    __shared__ int last;
     const int n = K + with_extra;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, c = blockIdx.x;
     const int L = J + 1, P = L * N;
     const size_t JN = (size_t)J * N;
-    double* stage = sh;                                        // [per][L][N]
-    double* part = sh + (size_t)per * P;                       // [per][L] chain sums
-    double* costs = part + (size_t)per * L;                    // [n]
-    int* sel = (int*)(costs + n);                              // [Kr]
-    for (int c0 = 0; c0 < n; c0 += per) {
-        const int nc = min(per, n - c0);
-        // every load of the chunk in flight (up to 16 candidates per batch), then the LDS stores
-        constexpr int kMaxLoads = 16;
-        for (int i = tid; i < P; i += kReuseBlock) {
-            const bool st = i < N;
-            for (int cb = 0; cb < nc; cb += kMaxLoads) {
-                double v[kMaxLoads];
+    {
+        double* stage = sh;   // [L][N]
+        constexpr int kMaxLoads = 4;
+        for (int i0 = tid; i0 < P; i0 += kMaxLoads * kReuseBlock) {
+            double v[kMaxLoads];
 #pragma unroll
-                for (int u = 0; u < kMaxLoads; ++u) {
-                    const int c = c0 + min(cb + u, nc - 1);
-                    const double* row = st ? (c < K ? src_state + (size_t)c * N : x_state) + i
-                                           : (c < K ? control + (size_t)c * JN : x_control) + (i - N);
-                    v[u] = *row;
-                }
-#pragma unroll
-                for (int u = 0; u < kMaxLoads; ++u)
-                    if (cb + u < nc) stage[(size_t)(cb + u) * P + i] = v[u];
+            for (int u = 0; u < kMaxLoads; ++u) {
+                const int i = min(i0 + u * kReuseBlock, P - 1);
+                v[u] = i < N ? (c < K ? src_state + (size_t)c * N : x_state)[i]
+                             : (c < K ? control + (size_t)c * JN : x_control)[i - N];
             }
+#pragma unroll
+            for (int u = 0; u < kMaxLoads; ++u)
+                if (i0 + u * kReuseBlock < P) stage[i0 + u * kReuseBlock] = v[u];
         }
         __syncthreads();
-        // chain_sum's order: x = v[0], then x += v[t] for t ascending
-        for (int it = tid; it < nc * L; it += kReuseBlock) {
-            const double* v = stage + (size_t)it * N;
+        if (tid < L) {
+            // chain_sum's order: x = v[0], then x += v[t] for t ascending
+            const double* v = stage + (size_t)tid * N;
             double x = v[0];
             for (int t0 = 1; t0 < N; t0 += 16) {
                 double b[16];
@@ -214,27 +206,34 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int per, int K, int J, in
                 for (int u = 0; u < 16; ++u)
                     if (t0 + u < N) x += b[u];
             }
-            part[it] = x;
+            part[tid] = x;
         }
         __syncthreads();
-        for (int cl = tid; cl < nc; cl += kReuseBlock) {
-            const double* q = part + (size_t)cl * L;
-            double s2 = q[0];
-            for (int d = 0; d < J; ++d) s2 += q[1 + d];
-            costs[c0 + cl] = s2 != s2 ? __builtin_inf() : s2;   // NaN ranks last: the ranks stay a permutation
+        if (tid == 0) {
+            double s2 = part[0];
+            for (int d = 0; d < J; ++d) s2 += part[1 + d];
+            costs_g[c] = s2 != s2 ? __builtin_inf() : s2;   // NaN ranks last: the ranks stay a permutation
+            __threadfence();   // release: the total before the count
+            last = atomicAdd(count, 1) == n - 1;
         }
-        __syncthreads();   // the stage is reused by the next chunk
+        __syncthreads();
     }
-    for (int c = tid; c < n; c += kReuseBlock) {
-        const int ic = c < K ? c : -1;
-        const double cc = costs[c];
+    if (!last) return;
+    __threadfence();   // acquire: every candidate's total
+    double* costs = sh;                       // [n] (the stage is dead)
+    int* sel = (int*)(costs + n);             // [Kr]
+    for (int i = tid; i < n; i += kReuseBlock) costs[i] = costs_g[i];
+    __syncthreads();
+    for (int cc0 = tid; cc0 < n; cc0 += kReuseBlock) {
+        const int ic = cc0 < K ? cc0 : -1;
+        const double cc = costs[cc0];
         int rank = 0;
         for (int c2 = 0; c2 < n; ++c2) {
             const int ic2 = c2 < K ? c2 : -1;
             const double x = costs[c2];
             if (x < cc || (x == cc && ic2 < ic)) ++rank;
         }
-        if (rank < Kr) sel[rank] = c;
+        if (rank < Kr) sel[rank] = cc0;
     }
     __syncthreads();
     // the kept rows into rows K_gen.. of this iteration's set (the row sets are distinct buffers,
@@ -266,24 +265,25 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int per, int K, int J, in
             }
         }
     }
+    if (tid == 0) *count = 0;   // for the next launch (stream order)
 }
 
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                 const int* stop, hipStream_t s)
+                 double* costs_g, int* count, const int* stop, hipStream_t s)
 {
     // k_reuse copies straight from the source rows into rows K_gen..: an in-place call would read
     // rows this same loop already overwrote
     if (src_params == params || src_state == state) return -1;
-    const int n = K + with_extra, L = J + 1, P = L * N;
-    const size_t fixed = (size_t)n * sizeof(double) + (size_t)(Kr + 1) * sizeof(int) + 16;
-    if (fixed + (size_t)(P + L) * sizeof(double) > kReuseLds) return -2;
-    const int per = std::min(n, (int)((kReuseLds - fixed) / ((size_t)(P + L) * sizeof(double))));
-    const size_t lds = (size_t)per * (P + L) * sizeof(double) + fixed;
+    const int n = K + with_extra, P = (J + 1) * N;
+    const size_t rank_bytes = (size_t)n * sizeof(double) + (size_t)Kr * sizeof(int);
+    const size_t lds = std::max((size_t)P * sizeof(double), rank_bytes);
+    if (lds > kReuseLds) return -2;
     if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);
-    hipLaunchKernelGGL(k_reuse, dim3(1), dim3(kReuseBlock), lds, s, per, K, J, N, Kr, K_gen, with_extra, src_params, src_state,
-                       src_control, params, noise, state, x_params, x_state, x_control, theta, stop);
+    hipLaunchKernelGGL(k_reuse, dim3(n), dim3(kReuseBlock), lds, s, K, J, N, Kr, K_gen, with_extra, src_params,
+                       src_state, src_control, params, noise, state, x_params, x_state, x_control, theta, costs_g,
+                       count, stop);
     return 0;
 }
 

@@ -156,12 +156,63 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     STAMP(5);
 }
 
+// The reused rows of an iteration (policy_improvement.cpp:208-224: noise re-based on theta by
+// k_reuse), then computeProjectedNoise (:473-482) and computeControlCosts: one 256-lane workgroup
+// per row and all its joints, M eps on the fp64 matrix cores (mfma_tile: the k-ascending fma
+// chains of the rollout kernel's noise phase, band_product's sums bit for bit), x = params + M eps,
+// then rollout_control (control_term / control_cost's expressions)
+template <int NG>
+__global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_nr[];
+    if (a.stop && *a.stop) return;
+    const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J), NB = N + kBandBatch;
+    const int r = a.row_begin + blockIdx.x;
+    const size_t row = (size_t)r * J * N;
+    double* eps = lds_nr;              // [NB][JP], zero rows past N and zero columns past J
+    double* xs = eps + NB * JP;        // [J][Nall]
+    double* cs = xs + J * Nall;        // [J][Nall]
+    const int tid = threadIdx.x;
+    for (int idx = tid; idx < NB * JP; idx += 256) {
+        const int k = idx / JP, d = idx - k * JP;
+        if (k >= N || d >= J) eps[idx] = 0.0;
+    }
+    for (int idx = tid; idx < J * N; idx += 256) {   // coalesced row reads
+        const int d = idx / N, k = idx - d * N;
+        eps[k * JP + d] = a.noise[row + idx];
+    }
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;
+    const int nti = (N + 15) >> 4;
+    const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
+    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
+    for (int ti = wv; ti < nti; ti += 4) {
+        double acc[NG];
+        mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
+        const int i = 16 * ti + irow;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
+            if (i < N && d < J) xs[d * Nall + i + 6] = a.params[row + (size_t)d * N + i] + acc[g];
+        }
+    }
+    rollout_control<256>(a, row, xs, cs, tid);
+}
+
 STOMP_STAMP_ACCESSORS(noise)
 
 void launch_noise(const NoiseArgs& a, hipStream_t s)
 {
     const int rows = a.K_loc - a.row_begin;
     if (rows <= 0) return;
+    if (!a.zero_noise && a.first_global + a.row_begin >= a.K_gen_global && a.J <= 4 * kNoiseJT) {
+        // every row is a reused one (no normals, no L z): the per-row matrix-core kernel
+        const size_t lds = ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall) * sizeof(double);
+        if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL(k_noise_rows<2>, dim3(rows), dim3(256), lds, s, a);
+        else hipLaunchKernelGGL(k_noise_rows<4>, dim3(rows), dim3(256), lds, s, a);
+        return;
+    }
     const int block = a.N <= 128 ? 128 : 256;
 #ifndef NOISE_RT
 #define NOISE_RT 4

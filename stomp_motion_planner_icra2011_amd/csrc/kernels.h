@@ -92,6 +92,8 @@ struct DevModel {
     double w_obs, w_con, w_tq;
     int pad_collision;
     const double* QT;           // [J][N][N]
+    int* split_cnt;             // [K_loc + 1] pieces done per rollout of the waypoint-split rollout
+                                // launch (zero between launches), null: no split launches
 };
 
 
@@ -206,6 +208,8 @@ struct CostArgs {
     double* x_ctl;
     double* x_prm;
     double* x_nse;
+    int split;                  // set by launch_cost: pieces per rollout of k_rollout_split
+    int* split_cnt;
 };
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
@@ -340,11 +344,12 @@ void launch_pad_fk(const DevModel& m, const double* start, const double* goal, d
 // src_*: the previous iteration's rows (ranked, copied from); params / noise / state: this
 // iteration's rows K_gen.. (written).  The two row sets must be distinct buffers (the copy has no
 // staging pass); returns -1 without launching when they alias, -2 when one candidate's cost rows
-// do not fit the LDS.
+// (or the ranking's totals) do not fit the LDS.  costs_g: [K + 1] scratch totals, count: a
+// counter that is zero between launches (the last workgroup resets it).
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                 const int* stop, hipStream_t s);
+                 double* costs_g, int* count, const int* stop, hipStream_t s);
 // sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
 // noise = eps, params = theta_gen + eps of rows left in a pregen buffer (rows_in_pre)
 void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,

@@ -290,6 +290,28 @@ def test_golden_cfg1_optimize():
     assert st.best_cost == g["best_cost"][0]
 
 
+@pytest.mark.parametrize("pieces", [1, 2, 3, 8, 40])
+@pytest.mark.parametrize("K,Kr,dof", [(20, 10, 7), (64, 0, 7), (16, 0, 14)])
+def test_waypoint_split_pieces_bitwise(monkeypatch, pieces, K, Kr, dof):
+    # k_rollout_split: a rollout's waypoints over `pieces` workgroups (1: the phased one-workgroup
+    # body), the velocity halo, the per-joint control rows dealt over the pieces, the last
+    # piece's costs.sum() and collision flag: the oracle's rows and totals bit for bit
+    monkeypatch.setenv("STOMP_DEBUG_SPLIT_MAX", str(pieces))
+    p = make(dof=dof, K=K, Kr=Kr, grid_n=64)
+    o, e = po.Oracle(p), eng.Engine(p)
+    for it in range(1, 5):
+        _compare_iteration(o, e, it)
+    # a batch of rows through stomp_engine_eval (per-rollout totals and flags: every piece counts)
+    rng = np.random.default_rng(pieces)
+    rows = o.theta()[None] + 0.3 * rng.standard_normal((3,) + o.theta().shape)
+    costs, cf, traj = e.execute(rows, 3)
+    for i in range(3):
+        co, cfo, tro = o.execute(rows[i], 3)
+        np.testing.assert_array_equal(costs[i], co)
+        np.testing.assert_array_equal(traj[i], tro)
+        assert bool(cf[i]) == cfo
+
+
 def test_golden_execute_cases():
     g = _golden("execute_cases")
     for dof in (7, 14):

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turns the rocprofv3 --pmc passes of tools/gpu_pmc.sh into the per-launch traffic
+"""Turns the rocprofv3 --pmc passes of `tools/gpu.sh pmc` into the per-launch traffic
 summary bench.py reports as roofline.traffic.
 
 Counters (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are KiB per

@@ -2,7 +2,7 @@
 
 Needs the stamps library (python -m stomp_motion_planner_icra2011_amd._build --stamps); never
 used for timing claims (the stamps serialise the kernels they instrument).
-Usage: STOMP_ENGINE_LIB=.../libstomp_engine_stamps.so python tools/stamps.py [K] [grid] [dof]
+Usage: STOMP_ENGINE_LIB=.../libstomp_engine_stamps.so python tools/stamps.py [K] [grid] [dof] [K_r]
 """
 import ctypes as C
 import os
@@ -17,8 +17,9 @@ from stomp_motion_planner_icra2011_amd import problem as pb  # noqa: E402
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 G = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 DOF = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+KR = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 lib = eng.load_library()
-p = pb.make_problem(dof=DOF, grid_n=G, num_rollouts=K, num_reused_rollouts=0, build_grid=False)
+p = pb.make_problem(dof=DOF, grid_n=G, num_rollouts=K, num_reused_rollouts=KR, build_grid=False)
 sdf = eng.DeviceBuffer(4 * G ** 3)
 eng.sdf_build_device(p, sdf.ptr)
 e = eng.Engine(p, sdf_device_ptr=sdf.ptr)
@@ -48,7 +49,14 @@ def show(name, block, labels):
         prev = v[i]
 
 
+SPLIT_LABELS = {200: "start", 201: "row loads + tables", 202: "row (noise / from pregen)", 203: "joint limits",
+                204: "traj out + sin/cos", 205: "FK (+ control rows)", 206: "pairs", 207: "velocities",
+                208: "fold + stores", 209: "count / last piece"}
+
+
 def cost_label(i):
+    if i in SPLIT_LABELS:
+        return "split: " + SPLIT_LABELS[i]
     if i in (61, 62, 63):
         return {61: "control terms (thread 0)", 62: "control terms barrier", 63: "control costs stored (t0)"}[i]
     if 100 <= i < 140:
@@ -77,7 +85,7 @@ def residency():
     e.run(7, 1)
     e.synchronize()
     fn(buf.ctypes.data)
-    b = buf[: K + 1].astype(np.int64)
+    b = buf[: int(os.environ.get("STAMP_BLOCKS", K + 1))].astype(np.int64)
     cu = ((b[:, 1] & 0xF) << 8) | ((b[:, 0] >> 8) & 0xFF)
     t0, t1 = b[:, 2], b[:, 3]
     import collections

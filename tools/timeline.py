@@ -1,4 +1,4 @@
-"""Kernel timeline of a rocprofv3 kernel trace (tools/gpu_trace.sh): the last `n` iterations,
+"""Kernel timeline of a rocprofv3 kernel trace (rocprofv3 --kernel-trace): the last `n` iterations,
 each dispatch's start relative to the first and its duration, in microseconds."""
 import csv
 import sys
