@@ -17,6 +17,8 @@
 #   art R [ARGS]             round artifacts of one workload: prof + pmc + tools/pmc_traffic.py
 #                            summary (gpurun_out/art_R/traffic.json) + its bench line
 #   final R                  tests + smoke + art R for cfg2 + the driver-shape bench line
+#   round R                  final R, then art R_cfgX for cfg1 / cfg3 / cfg4 / cfg5 and the
+#                            per-rank compute of the sharded shapes (gather 8 4 2, split 64 128 256)
 #   stamps LIB K [GRID DOF]  in-kernel phase stamps (tools/stamps.py) with the stamps library LIB
 #   gather W ...             gather-mode ranks on one GPU (STOMP_DEBUG_GATHER_RANKS=W), cfg2
 #   split K ...              the sharded weights phases at per-rank K (STOMP_DEBUG_SHARDED_MODES)
@@ -101,6 +103,15 @@ final)
   bash tools/gpu.sh art $r || exit 1
   bench_to gpurun_out/art_$r/bench_driver.json 500 --steps 20 --warmup 5 || exit 1
   cat gpurun_out/art_$r/bench_driver.json ;;
+round)
+  r=$1
+  bash tools/gpu.sh final $r || exit 1
+  bash tools/gpu.sh art ${r}_cfg1 --workload cfg1 --steps 200 --warmup 20 || exit 1
+  bash tools/gpu.sh art ${r}_cfg4 --workload cfg4 --steps 60 --warmup 10 || exit 1
+  bash tools/gpu.sh art ${r}_cfg3 --workload cfg3 --steps 20 --warmup 5 || exit 1
+  bash tools/gpu.sh art ${r}_cfg5 --workload cfg5 --steps 20 --warmup 5 || exit 1
+  bash tools/gpu.sh gather 8 4 2 || exit 1
+  bash tools/gpu.sh split 64 128 256 || exit 1 ;;
 stamps)
   lib=$1; k=$2; shift 2
   mkdir -p gpurun_out/stamps
