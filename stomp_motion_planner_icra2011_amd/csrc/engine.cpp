@@ -707,14 +707,16 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     const int g0 = e->first, g1 = std::min(e->first + e->K_loc, e->K_gen);
     const int num_gen = std::max(g1 - g0, 0);
     if (fused) na.row_begin = e->gather ? e->rows : num_gen;
-    // every local row generated (K_r = 0): eps and M eps come from k_pregen
-    const bool pre = fused && e->pre_on && num_gen == e->K_loc;
+    // the generated rows' eps and M eps come from the pregen buffers (every local row, or with
+    // reuse on one device the rows before the reused ones)
+    const bool pre = fused && e->pre_on && (num_gen == e->K_loc || (e->Kr > 0 && num_gen > 0));
     if (e->gather && !pre) return fail(e, STOMP_E_INVALID, "gather mode needs the pregen rows");
-    // outside the optimize loop the rows stay in the pregen buffer: the weights read eps there
-    // and nothing else needs the noise / params rows on the device (reuse is off with pregen).
-    // The optimize loop keeps the copies: after its stop the pregen blocks of the iterations
-    // enqueued past it still overwrite the buffers.
-    const bool rows_pre = pre && !e->tracking;
+    // outside the optimize loop and without reuse the rows stay in the pregen buffer: the weights
+    // read eps there and nothing else needs the noise / params rows on the device (the reuse step
+    // ranks and copies the previous rows, so with K_r > 0 they are written).  The optimize loop
+    // keeps the copies: after its stop the pregen blocks of the iterations enqueued past it still
+    // overwrite the buffers.
+    const bool rows_pre = pre && !e->tracking && e->Kr == 0;
     na.rows_in_pre = rows_pre ? 1 : 0;
     if (!rows_pre) e->rows_in_pre = false;
     if (pre) {
@@ -740,7 +742,7 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             ca.pre_rows = e->rows;
             ca.pre_next = pregen_args(e, it + 1);
             ca.ctl_by_pre = 1;
-            ca.ctl_rows = e->rows;
+            ca.ctl_rows = e->Kr > 0 ? num_gen : e->rows;   // the reused rows are priced by k_noise
             ca.row0 = e->row0;
             ca.state_out = e->d_state + (size_t)e->row0 * e->N;
             e->pre_it = it + 1;
@@ -941,7 +943,9 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         rc = fail(e, STOMP_E_INVALID, "at most %d rollouts per device", kSumBlock * 64);
         g_last_error = e->err; release(e); delete e; return rc;
     }
-    e->pre_on = e->Kr == 0 && e->J <= 16;   // the fused noise phase (rollout_project) takes J <= 16
+    // rows made ahead by the previous rollout launch (the fused noise phase takes J <= 16); with
+    // reused rollouts on one device too (the generated rows' noise does not depend on the reuse)
+    e->pre_on = (e->Kr == 0 || world == 1) && e->J <= 16;
     {
         // the K-sharded decomposition.  gather: one all-gather of the state-cost rows
         // per iteration, every rank making and pricing all K noise rows; partials: three exchanges
