@@ -1,6 +1,7 @@
 // k_misc.hip -- setup-time and bookkeeping kernels: padding-point FK, rollout reuse,
 // distance-field construction.
 #include "device_fk.h"
+#include "stamps.h"
 
 #include <algorithm>
 
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
     const int tid = threadIdx.x, c = blockIdx.x;
     const int L = J + 1, P = L * N;
     const size_t JN = (size_t)J * N;
+    STAMP(0);
     {
         double* stage = sh;   // [L][N]
         constexpr int kMaxLoads = 4;
@@ -194,6 +196,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
                 if (i0 + u * kReuseBlock < P) stage[i0 + u * kReuseBlock] = v[u];
         }
         __syncthreads();
+        STAMP(1);
         if (tid < L) {
             // chain_sum's order: x = v[0], then x += v[t] for t ascending
             const double* v = stage + (size_t)tid * N;
@@ -209,6 +212,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
             part[tid] = x;
         }
         __syncthreads();
+        STAMP(2);
         if (tid == 0) {
             double s2 = part[0];
             for (int d = 0; d < J; ++d) s2 += part[1 + d];
@@ -217,13 +221,16 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
             last = atomicAdd(count, 1) == n - 1;
         }
         __syncthreads();
+        STAMP(3);
     }
     if (!last) return;
+    STAMP_ANY(10);
     __threadfence();   // acquire: every candidate's total
     double* costs = sh;                       // [n] (the stage is dead)
     int* sel = (int*)(costs + n);             // [Kr]
     for (int i = tid; i < n; i += kReuseBlock) costs[i] = costs_g[i];
     __syncthreads();
+    STAMP_ANY(11);
     for (int cc0 = tid; cc0 < n; cc0 += kReuseBlock) {
         const int ic = cc0 < K ? cc0 : -1;
         const double cc = costs[cc0];
@@ -236,6 +243,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
         if (rank < Kr) sel[rank] = cc0;
     }
     __syncthreads();
+    STAMP_ANY(12);
     // the kept rows into rows K_gen.. of this iteration's set (the row sets are distinct buffers,
     // launch_reuse checks it): params row, noise = params - theta, state row; all loads of a batch
     // in flight before its stores
@@ -266,6 +274,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
         }
     }
     if (tid == 0) *count = 0;   // for the next launch (stream order)
+    STAMP_ANY(13);
 }
 
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
@@ -511,5 +520,7 @@ void launch_sdf_build(int nx, int ny, int nz, int cap2, const int* boxes, int nb
 {
     hipLaunchKernelGGL(k_sdf_build, dim3(2048), dim3(256), 0, s, nx, ny, nz, cap2, boxes, nb, cyl_d2, cyl_z, nc, out);
 }
+
+STOMP_STAMP_ACCESSORS(misc)
 
 }  // namespace stomp

@@ -172,16 +172,35 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
     double* eps = lds_nr;              // [NB][JP], zero rows past N and zero columns past J
     double* xs = eps + NB * JP;        // [J][Nall]
     double* cs = xs + J * Nall;        // [J][Nall]
+    double* prm = cs + J * Nall;       // [J][N] the params row
     const int tid = threadIdx.x;
+    STAMP(0);
+    // the noise and params rows: every load of the workgroup in flight at once (coalesced)
+    constexpr int kRowLoads = 4;   // J N <= 4 * 256 per pass (J <= 8, N <= 128 in one pass)
+    for (int i0 = tid; i0 - tid < J * N; i0 += kRowLoads * 256) {
+        double ve[kRowLoads], vp[kRowLoads];
+#pragma unroll
+        for (int u = 0; u < kRowLoads; ++u) {
+            const int idx = min(i0 + u * 256, J * N - 1);
+            ve[u] = a.noise[row + idx];
+            vp[u] = a.params[row + idx];
+        }
+#pragma unroll
+        for (int u = 0; u < kRowLoads; ++u) {
+            const int idx = i0 + u * 256;
+            if (idx < J * N) {
+                const int d = idx / N, k = idx - d * N;
+                eps[k * JP + d] = ve[u];
+                prm[idx] = vp[u];
+            }
+        }
+    }
     for (int idx = tid; idx < NB * JP; idx += 256) {
         const int k = idx / JP, d = idx - k * JP;
         if (k >= N || d >= J) eps[idx] = 0.0;
     }
-    for (int idx = tid; idx < J * N; idx += 256) {   // coalesced row reads
-        const int d = idx / N, k = idx - d * N;
-        eps[k * JP + d] = a.noise[row + idx];
-    }
     __syncthreads();
+    STAMP(1);
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;
     const int nti = (N + 15) >> 4;
@@ -194,10 +213,12 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const int d = 4 * g + jcol;
-            if (i < N && d < J) xs[d * Nall + i + 6] = a.params[row + (size_t)d * N + i] + acc[g];
+            if (i < N && d < J) xs[d * Nall + i + 6] = prm[d * N + i] + acc[g];
         }
     }
+    STAMP(2);
     rollout_control<256>(a, row, xs, cs, tid);
+    STAMP(5);
 }
 
 STOMP_STAMP_ACCESSORS(noise)
@@ -208,7 +229,8 @@ void launch_noise(const NoiseArgs& a, hipStream_t s)
     if (rows <= 0) return;
     if (!a.zero_noise && a.first_global + a.row_begin >= a.K_gen_global && a.J <= 4 * kNoiseJT) {
         // every row is a reused one (no normals, no L z): the per-row matrix-core kernel
-        const size_t lds = ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall) * sizeof(double);
+        const size_t lds = ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall + (size_t)a.J * a.N) *
+                           sizeof(double);
         if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL(k_noise_rows<2>, dim3(rows), dim3(256), lds, s, a);
         else hipLaunchKernelGGL(k_noise_rows<4>, dim3(rows), dim3(256), lds, s, a);
         return;

@@ -20,6 +20,17 @@ static __device__ int g_stamp_block;
         }                                                                                               \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
+// the same from whichever workgroup executes it (e.g. the last-arriving one of a launch)
+#define STAMP_ANY(i)                                                                                    \
+    do {                                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+        if (threadIdx.x == 0) {                                                                         \
+            unsigned long long _t;                                                                      \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                 \
+            g_stamps[(i)] = _t;                                                                         \
+        }                                                                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+    } while (0)
 // Per-workgroup residency record: {HW_ID, XCC_ID, start, end} for blocks < 8192, to measure
 // how many workgroups of a launch actually share a CU.
 static __device__ unsigned long long g_blocks[8192][6];
@@ -68,6 +79,9 @@ static __device__ unsigned long long g_blocks[8192][6];
 #else
 #define STAMP(i) \
     do {         \
+    } while (0)
+#define STAMP_ANY(i) \
+    do {             \
     } while (0)
 #define BLOCK_BEGIN() \
     do {              \

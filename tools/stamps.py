@@ -73,7 +73,14 @@ def cost_label(i):
 show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch (odd: FK on waves 2-3)
 show("cost", 2, cost_label)   # an even one (FK on waves 0-1, thread 0 stamps inside the FK lanes)
 show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
-show("noise", 0, lambda i: ["start", "normals", "L z", "M eps", "control", "end"][i])
+NOISE_LABELS = {0: "start", 1: "rows loaded / normals", 2: "M eps (rows) / L z", 3: "M eps", 4: "control", 5: "end",
+                9: "control: padding", 61: "control terms (thread 0)", 62: "control terms barrier",
+                63: "control costs stored (t0)"}
+show("noise", 0, lambda i: NOISE_LABELS.get(i, str(i)))
+if KR > 0:
+    show("misc", 0, lambda i: {0: "k_reuse: start", 1: "rows staged", 2: "t-chains", 3: "total counted",
+                               10: "last: start", 11: "last: totals loaded", 12: "last: ranked",
+                               13: "last: rows copied"}.get(i, str(i)))
 show("weights", 0, lambda i: ["start", "min/max", "exp", "psum", "u partials", "end", "tile loaded"][i])
 
 
