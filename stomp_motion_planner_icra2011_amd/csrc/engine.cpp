@@ -750,7 +750,11 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
-            ca.x_state = e->d_x_state; ca.x_cf = e->d_cf; ca.x_traj = e->d_last_traj; ca.x_total = e->d_total;
+            ca.x_state = e->d_x_state; ca.x_traj = e->d_last_traj;
+            // the pipelined noiseless rollout's costs.sum() and collision flag are read only by
+            // the optimize loop's bookkeeping (k_track); stomp_engine_iterate and the flush
+            // evaluate their own, so without tracking the launch skips them
+            if (e->tracking) { ca.x_cf = e->d_cf; ca.x_total = e->d_total; }
             if (e->Kr > 0) { ca.x_ctl = e->d_x_control; ca.x_prm = e->d_x_params; ca.x_nse = e->d_x_noise; }
             e->pending_member = -1;
         }

@@ -198,16 +198,25 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
         __syncthreads();
         STAMP(1);
         if (tid < L) {
-            // chain_sum's order: x = v[0], then x += v[t] for t ascending
+            // chain_sum's order: x = v[0], then x += v[t] for t ascending; the next 16 values
+            // are read while this 16 are added (two buffers that swap roles, no copies)
             const double* v = stage + (size_t)tid * N;
             double x = v[0];
-            for (int t0 = 1; t0 < N; t0 += 16) {
-                double b[16];
+            double b0[16], b1[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) b[u] = v[min(t0 + u, N - 1)];
+            for (int u = 0; u < 16; ++u) b0[u] = v[min(1 + u, N - 1)];
+            for (int t0 = 1; t0 < N; t0 += 32) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) b1[u] = v[min(t0 + 16 + u, N - 1)];
 #pragma unroll
                 for (int u = 0; u < 16; ++u)
-                    if (t0 + u < N) x += b[u];
+                    if (t0 + u < N) x += b0[u];
+                if (t0 + 16 >= N) break;
+#pragma unroll
+                for (int u = 0; u < 16; ++u) b0[u] = v[min(t0 + 32 + u, N - 1)];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (t0 + 16 + u < N) x += b1[u];
             }
             part[tid] = x;
         }
@@ -235,10 +244,15 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
         const int ic = cc0 < K ? cc0 : -1;
         const double cc = costs[cc0];
         int rank = 0;
-        for (int c2 = 0; c2 < n; ++c2) {
-            const int ic2 = c2 < K ? c2 : -1;
-            const double x = costs[c2];
-            if (x < cc || (x == cc && ic2 < ic)) ++rank;
+        for (int c0 = 0; c0 < n; c0 += 8) {   // eight reads in flight, then the compares
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = costs[min(c0 + u, n - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int c2 = c0 + u, ic2 = c2 < K ? c2 : -1;
+                if (c2 < n && (x[u] < cc || (x[u] == cc && ic2 < ic))) ++rank;
+            }
         }
         if (rank < Kr) sel[rank] = cc0;
     }

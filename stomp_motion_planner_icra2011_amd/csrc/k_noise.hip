@@ -157,12 +157,12 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 }
 
 // The reused rows of an iteration (policy_improvement.cpp:208-224: noise re-based on theta by
-// k_reuse), then computeProjectedNoise (:473-482) and computeControlCosts: one 256-lane workgroup
+// k_reuse), then computeProjectedNoise (:473-482) and computeControlCosts: one workgroup
 // per row and all its joints, M eps on the fp64 matrix cores (mfma_tile: the k-ascending fma
 // chains of the rollout kernel's noise phase, band_product's sums bit for bit), x = params + M eps,
 // then rollout_control (control_term / control_cost's expressions)
-template <int NG>
-__global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
+template <int BLOCK, int NG>
+__global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double lds_nr[];
     if (a.stop && *a.stop) return;
@@ -176,18 +176,18 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
     const int tid = threadIdx.x;
     STAMP(0);
     // the noise and params rows: every load of the workgroup in flight at once (coalesced)
-    constexpr int kRowLoads = 4;   // J N <= 4 * 256 per pass (J <= 8, N <= 128 in one pass)
-    for (int i0 = tid; i0 - tid < J * N; i0 += kRowLoads * 256) {
+    constexpr int kRowLoads = 4096 / BLOCK;   // the row in few passes
+    for (int i0 = tid; i0 - tid < J * N; i0 += kRowLoads * BLOCK) {
         double ve[kRowLoads], vp[kRowLoads];
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
-            const int idx = min(i0 + u * 256, J * N - 1);
+            const int idx = min(i0 + u * BLOCK, J * N - 1);
             ve[u] = a.noise[row + idx];
             vp[u] = a.params[row + idx];
         }
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
-            const int idx = i0 + u * 256;
+            const int idx = i0 + u * BLOCK;
             if (idx < J * N) {
                 const int d = idx / N, k = idx - d * N;
                 eps[k * JP + d] = ve[u];
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
             }
         }
     }
-    for (int idx = tid; idx < NB * JP; idx += 256) {
+    for (int idx = tid; idx < NB * JP; idx += BLOCK) {
         const int k = idx / JP, d = idx - k * JP;
         if (k >= N || d >= J) eps[idx] = 0.0;
     }
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
     const int nti = (N + 15) >> 4;
     const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
     const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
-    for (int ti = wv; ti < nti; ti += 4) {
+    for (int ti = wv; ti < nti; ti += BLOCK / 64) {
         double acc[NG];
         mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
         const int i = 16 * ti + irow;
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void k_noise_rows(NoiseArgs a)
         }
     }
     STAMP(2);
-    rollout_control<256>(a, row, xs, cs, tid);
+    rollout_control<BLOCK>(a, row, xs, cs, tid);
     STAMP(5);
 }
 
@@ -231,8 +231,14 @@ void launch_noise(const NoiseArgs& a, hipStream_t s)
         // every row is a reused one (no normals, no L z): the per-row matrix-core kernel
         const size_t lds = ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall + (size_t)a.J * a.N) *
                            sizeof(double);
-        if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL(k_noise_rows<2>, dim3(rows), dim3(256), lds, s, a);
-        else hipLaunchKernelGGL(k_noise_rows<4>, dim3(rows), dim3(256), lds, s, a);
+        // one wave per 16-waypoint tile of the projection (N <= 128: 8 waves)
+        if (a.N <= 128) {
+            if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL((k_noise_rows<512, 2>), dim3(rows), dim3(512), lds, s, a);
+            else hipLaunchKernelGGL((k_noise_rows<512, 4>), dim3(rows), dim3(512), lds, s, a);
+        } else {
+            if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL((k_noise_rows<1024, 2>), dim3(rows), dim3(1024), lds, s, a);
+            else hipLaunchKernelGGL((k_noise_rows<1024, 4>), dim3(rows), dim3(1024), lds, s, a);
+        }
         return;
     }
     const int block = a.N <= 128 ? 128 : 256;
