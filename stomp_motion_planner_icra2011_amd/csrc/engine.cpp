@@ -775,11 +775,32 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         if (int rc = exchange_state(e)) return rc;
     if (reuse_late) {
         // the previous rows and the extra rollout (evaluated just now) ranked; the reused rows'
-        // projection and control costs after them
-        if (int rc = run_reuse(e)) return rc;
-        if (na.row_begin < na.K_loc) {
+        // projection and control costs after them.  On one device the candidates' totals are
+        // made by k_reuse and the reused rows' kernel ranks, copies and prices each row itself
+        if (e->world == 1 && launch_reuse_rows_ok(na, e->K, e->Kr)) {
+            ReuseArgs ra{};
+            ra.K = e->K; ra.Kr = e->Kr; ra.K_gen = e->K_gen; ra.with_extra = e->extra_added ? 1 : 0;
+            e->extra_added = false;
+            ra.costs = e->d_reuse_costs;
+            ra.src_params = e->d_params_b; ra.src_state = e->d_state_b;
+            ra.x_params = e->d_x_params; ra.x_state = e->d_x_state; ra.state = e->d_state;
+            {
+                Timed tm(e, T_REUSE);
+                if (int rc = launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, ra.with_extra, e->d_params_b, e->d_state_b,
+                                          e->d_control_b, e->d_params, e->d_noise, e->d_state, e->d_x_params,
+                                          e->d_x_state, e->d_x_control, e->d_theta, e->d_reuse_costs, e->d_reuse_count,
+                                          e->d_stop, e->stream, true))
+                    return fail(e, STOMP_E_INVALID, rc == -1 ? "reuse: the source and destination rollout rows alias"
+                                                             : "reuse: the cost rows of one candidate exceed the LDS");
+            }
             Timed tm(e, T_NOISE);
-            launch_noise(na, e->stream);
+            launch_reuse_rows(na, ra, e->stream);
+        } else {
+            if (int rc = run_reuse(e)) return rc;
+            if (na.row_begin < na.K_loc) {
+                Timed tm(e, T_NOISE);
+                launch_noise(na, e->stream);
+            }
         }
     }
     WeightArgs wa{};

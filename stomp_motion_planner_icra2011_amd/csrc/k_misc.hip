@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
                                                        const double* control, double* params, double* noise,
                                                        double* state, const double* x_params, const double* x_state,
                                                        const double* x_control, const double* theta, double* costs_g,
-                                                       int* count, const int* stop)
+                                                       int* count, const int* stop, int costs_only)
 {
     if (stop && *stop) return;
     extern __shared__ __attribute__((aligned(16))) double sh[];
@@ -226,8 +226,12 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
             double s2 = part[0];
             for (int d = 0; d < J; ++d) s2 += part[1 + d];
             costs_g[c] = s2 != s2 ? __builtin_inf() : s2;   // NaN ranks last: the ranks stay a permutation
-            __threadfence();   // release: the total before the count
-            last = atomicAdd(count, 1) == n - 1;
+            if (!costs_only) {
+                __threadfence();   // release: the total before the count
+                last = atomicAdd(count, 1) == n - 1;
+            } else {
+                last = 0;   // the ranking and copies are the reused rows' kernel's (launch_reuse_rows)
+            }
         }
         __syncthreads();
         STAMP(3);
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(kReuseBlock) void k_reuse(int K, int J, int N, int 
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                 double* costs_g, int* count, const int* stop, hipStream_t s)
+                 double* costs_g, int* count, const int* stop, hipStream_t s, bool costs_only)
 {
     // k_reuse copies straight from the source rows into rows K_gen..: an in-place call would read
     // rows this same loop already overwrote
@@ -306,7 +310,7 @@ int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const d
     if (lds > 48 * 1024) lds_opt_in((const void*)k_reuse, lds);
     hipLaunchKernelGGL(k_reuse, dim3(n), dim3(kReuseBlock), lds, s, K, J, N, Kr, K_gen, with_extra, src_params,
                        src_state, src_control, params, noise, state, x_params, x_state, x_control, theta, costs_g,
-                       count, stop);
+                       count, stop, costs_only ? 1 : 0);
     return 0;
 }
 

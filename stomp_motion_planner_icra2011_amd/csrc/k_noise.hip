@@ -156,15 +156,20 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     STAMP(5);
 }
 
-// The reused rows of an iteration (policy_improvement.cpp:208-224: noise re-based on theta by
-// k_reuse), then computeProjectedNoise (:473-482) and computeControlCosts: one workgroup
-// per row and all its joints, M eps on the fp64 matrix cores (mfma_tile: the k-ascending fma
-// chains of the rollout kernel's noise phase, band_product's sums bit for bit), x = params + M eps,
-// then rollout_control (control_term / control_cost's expressions)
-template <int BLOCK, int NG>
-__global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a)
+// The reused rows of an iteration (policy_improvement.cpp:208-224: noise re-based on theta),
+// then computeProjectedNoise (:473-482) and computeControlCosts: one workgroup per row and all its
+// joints (BLOCK / 64 waves >= the row's 16-waypoint tiles: one round), M eps on the fp64 matrix
+// cores (mfma_tile: the k-ascending fma chains of the rollout kernel's noise phase, band_product's
+// sums bit for bit), x = params + M eps, then rollout_control (control_term / control_cost's
+// expressions).  REUSE: the row is not copied yet; the workgroup of reused row rr ranks the
+// candidates from their totals (k_reuse's (cost, index) order, the extra rollout at -1), takes
+// the candidate of rank rr and writes its params, the noise params - theta and its state row
+// (k_reuse's copy), then prices it from registers and LDS.
+template <int BLOCK, int NG, bool REUSE>
+__global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
 {
     extern __shared__ __attribute__((aligned(16))) double lds_nr[];
+    __shared__ int src_sel;
     if (a.stop && *a.stop) return;
     const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J), NB = N + kBandBatch;
     const int r = a.row_begin + blockIdx.x;
@@ -175,6 +180,35 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a)
     double* prm = cs + J * Nall;       // [J][N] the params row
     const int tid = threadIdx.x;
     STAMP(0);
+    const double* psrc = a.params + row;
+    const double* nsrc = a.noise + row;
+    if constexpr (REUSE) {
+        const int n = ra.K + ra.with_extra, rr = r - ra.K_gen;
+        double* costs = prm + J * N;   // [n]
+        for (int i = tid; i < n; i += BLOCK) costs[i] = ra.costs[i];
+        __syncthreads();
+        for (int c = tid; c < n; c += BLOCK) {
+            const int ic = c < ra.K ? c : -1;
+            const double cc = costs[c];
+            int rank = 0;
+            for (int c0 = 0; c0 < n; c0 += 8) {
+                double x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = costs[min(c0 + u, n - 1)];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int c2 = c0 + u, ic2 = c2 < ra.K ? c2 : -1;
+                    if (c2 < n && (x[u] < cc || (x[u] == cc && ic2 < ic))) ++rank;
+                }
+            }
+            if (rank == rr) src_sel = c;   // ranks are a permutation: one writer
+        }
+        __syncthreads();
+        const int src = src_sel;
+        psrc = src < ra.K ? ra.src_params + (size_t)src * J * N : ra.x_params;
+        const double* ssrc = src < ra.K ? ra.src_state + (size_t)src * N : ra.x_state;
+        for (int i = tid; i < N; i += BLOCK) ra.state[(size_t)r * N + i] = ssrc[i];
+    }
     // the noise and params rows: every load of the workgroup in flight at once (coalesced)
     constexpr int kRowLoads = 4096 / BLOCK;   // the row in few passes
     for (int i0 = tid; i0 - tid < J * N; i0 += kRowLoads * BLOCK) {
@@ -182,15 +216,21 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a)
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
             const int idx = min(i0 + u * BLOCK, J * N - 1);
-            ve[u] = a.noise[row + idx];
-            vp[u] = a.params[row + idx];
+            vp[u] = psrc[idx];
+            ve[u] = REUSE ? a.theta[idx] : nsrc[idx];
         }
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
             const int idx = i0 + u * BLOCK;
             if (idx < J * N) {
                 const int d = idx / N, k = idx - d * N;
-                eps[k * JP + d] = ve[u];
+                double e = ve[u];
+                if constexpr (REUSE) {
+                    e = vp[u] - ve[u];   // k_reuse's copy: params, noise = params - theta
+                    a.params[row + idx] = vp[u];
+                    a.noise[row + idx] = e;
+                }
+                eps[k * JP + d] = e;
                 prm[idx] = vp[u];
             }
         }
@@ -221,24 +261,59 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a)
     STAMP(5);
 }
 
+namespace {
+constexpr int kReuseRowsMax = 1024;   // candidates the reused rows' kernel ranks itself
+
+size_t noise_rows_lds(const NoiseArgs& a, int n)
+{
+    return ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall + (size_t)a.J * a.N + (size_t)n) *
+           sizeof(double);
+}
+
+template <int BLOCK, int NG, bool REUSE>
+void launch_noise_rows_t(const NoiseArgs& a, const ReuseArgs& ra, int rows, size_t lds, hipStream_t s)
+{
+    if (lds > 64 * 1024) lds_opt_in((const void*)k_noise_rows<BLOCK, NG, REUSE>, lds);
+    hipLaunchKernelGGL((k_noise_rows<BLOCK, NG, REUSE>), dim3(rows), dim3(BLOCK), lds, s, a, ra);
+}
+
+template <bool REUSE>
+void launch_noise_rows(const NoiseArgs& a, const ReuseArgs& ra, int rows, size_t lds, hipStream_t s)
+{
+    // one wave per 16-waypoint tile of the projection (N <= 128: 8 waves)
+    if (a.N <= 128) {
+        if (a.J <= 2 * kNoiseJT) launch_noise_rows_t<512, 2, REUSE>(a, ra, rows, lds, s);
+        else launch_noise_rows_t<512, 4, REUSE>(a, ra, rows, lds, s);
+    } else {
+        if (a.J <= 2 * kNoiseJT) launch_noise_rows_t<1024, 2, REUSE>(a, ra, rows, lds, s);
+        else launch_noise_rows_t<1024, 4, REUSE>(a, ra, rows, lds, s);
+    }
+}
+}  // namespace
+
+bool launch_reuse_rows_ok(const NoiseArgs& a, int K, int Kr)
+{
+    return !a.zero_noise && a.first_global == 0 && a.row_begin >= a.K_gen_global && a.K_loc - a.row_begin == Kr &&
+           a.J <= 4 * kNoiseJT && K + 1 <= kReuseRowsMax && noise_rows_lds(a, K + 1) <= kRolloutLdsMax;
+}
+
+void launch_reuse_rows(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s)
+{
+    const int rows = a.K_loc - a.row_begin;
+    if (rows <= 0) return;
+    launch_noise_rows<true>(a, ra, rows, noise_rows_lds(a, ra.K + ra.with_extra), s);
+}
+
 STOMP_STAMP_ACCESSORS(noise)
 
 void launch_noise(const NoiseArgs& a, hipStream_t s)
 {
     const int rows = a.K_loc - a.row_begin;
     if (rows <= 0) return;
-    if (!a.zero_noise && a.first_global + a.row_begin >= a.K_gen_global && a.J <= 4 * kNoiseJT) {
+    if (!a.zero_noise && a.first_global + a.row_begin >= a.K_gen_global && a.J <= 4 * kNoiseJT &&
+        noise_rows_lds(a, 0) <= kRolloutLdsMax) {
         // every row is a reused one (no normals, no L z): the per-row matrix-core kernel
-        const size_t lds = ((size_t)(a.N + kBandBatch) * noise_jp(a.J) + 2 * (size_t)a.J * a.Nall + (size_t)a.J * a.N) *
-                           sizeof(double);
-        // one wave per 16-waypoint tile of the projection (N <= 128: 8 waves)
-        if (a.N <= 128) {
-            if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL((k_noise_rows<512, 2>), dim3(rows), dim3(512), lds, s, a);
-            else hipLaunchKernelGGL((k_noise_rows<512, 4>), dim3(rows), dim3(512), lds, s, a);
-        } else {
-            if (a.J <= 2 * kNoiseJT) hipLaunchKernelGGL((k_noise_rows<1024, 2>), dim3(rows), dim3(1024), lds, s, a);
-            else hipLaunchKernelGGL((k_noise_rows<1024, 4>), dim3(rows), dim3(1024), lds, s, a);
-        }
+        launch_noise_rows<false>(a, ReuseArgs{}, rows, noise_rows_lds(a, 0), s);
         return;
     }
     const int block = a.N <= 128 ? 128 : 256;

@@ -289,6 +289,21 @@ size_t terms_lds_bytes(const TermsModel& m);
 void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
 
 void launch_noise(const NoiseArgs& a, hipStream_t s);
+// The reuse step with the reused rows' projection and control costs (policy_improvement.cpp:
+// 176-225, 473-482): candidate totals (launch_reuse with costs only), then one workgroup per
+// reused row ranks the candidates, copies the row of rank rr (params, noise re-based on theta,
+// state) and prices it.  Only when launch_reuse_rows_ok.
+struct ReuseArgs {
+    int K, Kr, K_gen, with_extra;
+    const double* costs;        // [K + with_extra] candidate totals (launch_reuse, costs only)
+    const double* src_params;   // the previous row set
+    const double* src_state;
+    const double* x_params;     // the extra (noiseless) rollout
+    const double* x_state;
+    double* state;              // this iteration's state rows (rows K_gen.. written)
+};
+bool launch_reuse_rows_ok(const NoiseArgs& a, int K, int Kr);
+void launch_reuse_rows(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s);
 // the theta-independent part of generateRollouts + computeProjectedNoise for rows [0, rows):
 // normals, eps = sigma L z and M eps into a.pre_eps / a.pre_meps (run ahead on a side stream)
 void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s);
@@ -349,7 +364,7 @@ void launch_pad_fk(const DevModel& m, const double* start, const double* goal, d
 int launch_reuse(int K, int J, int N, int Kr, int K_gen, int with_extra, const double* src_params,
                  const double* src_state, const double* src_control, double* params, double* noise, double* state,
                  const double* x_params, const double* x_state, const double* x_control, const double* theta,
-                 double* costs_g, int* count, const int* stop, hipStream_t s);
+                 double* costs_g, int* count, const int* stop, hipStream_t s, bool costs_only = false);
 // sharded reuse (world > 1): per-rank totals, the replicated ranking, pack / unpack of the slots
 // noise = eps, params = theta_gen + eps of rows left in a pregen buffer (rows_in_pre)
 void launch_materialize_rows(int K_loc, int JN, const double* eps, const double* theta_gen, double* noise,
