@@ -747,6 +747,11 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             ca.state_out = e->d_state + (size_t)e->row0 * e->N;
             e->pre_it = it + 1;
         }
+        if (reuse_late && e->world == 1 && launch_reuse_rows_ok(na, e->K, e->Kr)) {
+            // the reuse candidates' totals (the previous rows, complete) made beside the rollouts
+            ca.tot_rows = e->K;
+            ca.tot_state = e->d_state_b; ca.tot_control = e->d_control_b; ca.tot_out = e->d_reuse_costs;
+        }
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
         if (e->pending_member >= 0) {
             ca.x_params = e->d_theta; ca.x_member = e->pending_member;
@@ -783,16 +788,8 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             e->extra_added = false;
             ra.costs = e->d_reuse_costs;
             ra.src_params = e->d_params_b; ra.src_state = e->d_state_b;
-            ra.x_params = e->d_x_params; ra.x_state = e->d_x_state; ra.state = e->d_state;
-            {
-                Timed tm(e, T_REUSE);
-                if (int rc = launch_reuse(e->K, e->J, e->N, e->Kr, e->K_gen, ra.with_extra, e->d_params_b, e->d_state_b,
-                                          e->d_control_b, e->d_params, e->d_noise, e->d_state, e->d_x_params,
-                                          e->d_x_state, e->d_x_control, e->d_theta, e->d_reuse_costs, e->d_reuse_count,
-                                          e->d_stop, e->stream, true))
-                    return fail(e, STOMP_E_INVALID, rc == -1 ? "reuse: the source and destination rollout rows alias"
-                                                             : "reuse: the cost rows of one candidate exceed the LDS");
-            }
+            ra.x_params = e->d_x_params; ra.x_state = e->d_x_state; ra.x_control = e->d_x_control;
+            ra.state = e->d_state;
             Timed tm(e, T_NOISE);
             launch_reuse_rows(na, ra, e->stream);
         } else {

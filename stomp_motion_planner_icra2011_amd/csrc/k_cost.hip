@@ -259,6 +259,17 @@ __device__ __forceinline__ void pregen_block(const CostArgs& a, int r, bool own,
     }
 }
 
+// a rollout launch's block past its pregen blocks: the total of reuse candidate c (the previous
+// iteration's row c, candidate_total) for launch_reuse_rows; stage: (J + 1) N doubles of LDS
+template <int BLOCK>
+__device__ __forceinline__ void totals_block(const CostArgs& a, int J, int N, int c, double* stage)
+{
+    if (a.stop && *a.stop) return;
+    const double t = candidate_total<BLOCK>(a.tot_state + (size_t)c * N, a.tot_control + (size_t)c * J * N, J, N,
+                                            stage, threadIdx.x);
+    if (threadIdx.x == 0) a.tot_out[c] = t;
+}
+
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
 // FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
@@ -281,13 +292,17 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         const int nro = a.num_noisy + (a.x_params ? 1 : 0);
         if (bid >= nro) {
             const int r = bid - nro;
+            if (r >= a.pre_rows) {   // the reuse candidates' totals (nzA, nzB: contiguous)
+                totals_block<BLOCK>(a, J, N, r - a.pre_rows, (double*)(lds_raw + L.nzA));
+                return;
+            }
             // a phased launch's rollouts price their own rows (the FK-idle waves)
             const bool own = PHASED && r >= a.row0 && r < a.row0 + a.num_noisy;
             pregen_block<BLOCK>(a, r, own, (double*)(lds_raw + L.nzA), (double*)(lds_raw + L.nzB));
             return;
         }
     }
-    if (a.pre_rows > 0) __builtin_amdgcn_s_setprio(2);
+    if (a.pre_rows > 0 || a.tot_rows > 0) __builtin_amdgcn_s_setprio(2);
     if (a.stop && *a.stop) return;
     double* traj = (double*)(lds_raw + L.traj);   // J*N
     double* fb = (double*)(lds_raw + L.fb);       // 12*N frame of the current slot
@@ -898,10 +913,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
     double* zA = (double*)(lds_raw + L.zA);
     double* zB = (double*)(lds_raw + L.zB);
     if (bid >= nro * P) {
-        pregen_block<BLOCK>(a, bid - nro * P, false, zA, zB);
+        const int r = bid - nro * P;
+        if (r >= a.pre_rows) totals_block<BLOCK>(a, J, N, r - a.pre_rows, zA);   // zA, zB: contiguous
+        else pregen_block<BLOCK>(a, r, false, zA, zB);
         return;
     }
-    if (a.pre_rows > 0) __builtin_amdgcn_s_setprio(2);
+    if (a.pre_rows > 0 || a.tot_rows > 0) __builtin_amdgcn_s_setprio(2);
     if (a.stop && *a.stop) return;
     STAMP(200);
     BLOCK_BEGIN();
@@ -1337,18 +1354,19 @@ int rollout_blocks_per_cu(size_t lds_total)
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int nro = a.num_noisy + (a.x_params ? 1 : 0);
-    const int blocks = nro + (a.pre_rows > 0 ? a.pre_rows : 0);
+    const int extra_blocks = (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows;   // pregen, then totals
+    const int blocks = nro + extra_blocks;
     if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
-    if (const int P = split_pieces(m, nro, a.pre_rows > 0 ? a.pre_rows : 0)) {
+    if (const int P = split_pieces(m, nro, extra_blocks)) {
         const size_t ls = rollout_split_lds_bytes(m, P);
         if (ls + 1024 <= kRolloutLdsMax) {
             CostArgs b = a;
             b.split = P;
             b.split_cnt = m.split_cnt;
             lds_opt_in((const void*)k_rollout_split<kSplitBlock>, ls);
-            hipLaunchKernelGGL((k_rollout_split<kSplitBlock>), dim3(nro * P + (a.pre_rows > 0 ? a.pre_rows : 0)),
-                               dim3(kSplitBlock), ls, s, m, b);
+            hipLaunchKernelGGL((k_rollout_split<kSplitBlock>), dim3(nro * P + extra_blocks), dim3(kSplitBlock), ls, s, m,
+                               b);
             return;
         }
     }

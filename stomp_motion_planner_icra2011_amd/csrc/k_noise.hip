@@ -164,7 +164,8 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 // expressions).  REUSE: the row is not copied yet; the workgroup of reused row rr ranks the
 // candidates from their totals (k_reuse's (cost, index) order, the extra rollout at -1), takes
 // the candidate of rank rr and writes its params, the noise params - theta and its state row
-// (k_reuse's copy), then prices it from registers and LDS.
+// (k_reuse's copy), then prices it from registers and LDS.  The K previous rows' totals come from
+// the rollout launch's totals blocks; the extra rollout's is made here (candidate_total).
 template <int BLOCK, int NG, bool REUSE>
 __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
 {
@@ -184,8 +185,14 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
     const double* nsrc = a.noise + row;
     if constexpr (REUSE) {
         const int n = ra.K + ra.with_extra, rr = r - ra.K_gen;
-        double* costs = prm + J * N;   // [n]
-        for (int i = tid; i < n; i += BLOCK) costs[i] = ra.costs[i];
+        double* costs = prm + J * N;   // [n]: the K previous rows' totals (the rollout launch's), the extra's
+        for (int i = tid; i < ra.K; i += BLOCK) costs[i] = ra.costs[i];
+        if (ra.with_extra) {
+            // the extra (noiseless) rollout's total, evaluated by this iteration's rollout launch;
+            // xs and cs are its stage (dead until the projection)
+            const double t = candidate_total<BLOCK>(ra.x_state, ra.x_control, J, N, xs, tid);
+            if (tid == 0) costs[ra.K] = t;
+        }
         __syncthreads();
         for (int c = tid; c < n; c += BLOCK) {
             const int ic = c < ra.K ? c : -1;

@@ -210,6 +210,13 @@ struct CostArgs {
     double* x_nse;
     int split;                  // set by launch_cost: pieces per rollout of k_rollout_split
     int* split_cnt;
+    // blocks after the pregen ones: Rollout::getCost of the previous iteration's K rows (the reuse
+    // candidates, tot_state [K][N] / tot_control [K][J][N]) into tot_out [K] (launch_reuse_rows
+    // ranks them with the extra rollout's)
+    int tot_rows;
+    const double* tot_state;
+    const double* tot_control;
+    double* tot_out;
 };
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
@@ -290,9 +297,10 @@ void launch_terms(const TermsModel& m, const TermsArgs& a, hipStream_t s);
 
 void launch_noise(const NoiseArgs& a, hipStream_t s);
 // The reuse step with the reused rows' projection and control costs (policy_improvement.cpp:
-// 176-225, 473-482): candidate totals (launch_reuse with costs only), then one workgroup per
-// reused row ranks the candidates, copies the row of rank rr (params, noise re-based on theta,
-// state) and prices it.  Only when launch_reuse_rows_ok.
+// 176-225, 473-482): the K previous rows' totals made by the rollout launch (CostArgs::tot_*),
+// then one workgroup per reused row prices the extra rollout, ranks the candidates, copies the
+// row of rank rr (params, noise re-based on theta, state) and prices it.  Only when
+// launch_reuse_rows_ok.
 struct ReuseArgs {
     int K, Kr, K_gen, with_extra;
     const double* costs;        // [K + with_extra] candidate totals (launch_reuse, costs only)
@@ -300,6 +308,7 @@ struct ReuseArgs {
     const double* src_state;
     const double* x_params;     // the extra (noiseless) rollout
     const double* x_state;
+    const double* x_control;
     double* state;              // this iteration's state rows (rows K_gen.. written)
 };
 bool launch_reuse_rows_ok(const NoiseArgs& a, int K, int Kr);

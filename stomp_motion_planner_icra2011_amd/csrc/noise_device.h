@@ -612,6 +612,60 @@ __device__ __forceinline__ void pre_row_control(const NoiseArgs& a, int r, doubl
     rollout_control<BLOCK>(a, (size_t)r * JN, xs, cs, tid, nullptr);
 }
 
+// Rollout::getCost (policy_improvement.cpp:149-156) of one reuse candidate in k_reuse's order:
+// its state row and J control rows staged in LDS (stage: (J + 1) N doubles) with every load in
+// flight, one t-chain per row (x = v[0], then x += v[t] ascending), then part[0] + part[1] + ...
+// + part[J]; NaN as +inf (the ranks stay a permutation).  The whole block calls it; thread 0
+// gets the total.
+template <int BLOCK>
+__device__ __forceinline__ double candidate_total(const double* state, const double* control, int J, int N,
+                                                  double* stage, int tid)
+{
+    __shared__ double part[kMaxJoints + 1];
+    const int L = J + 1, P = L * N;
+    for (int i0 = tid; i0 - tid < P; i0 += 4 * BLOCK) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = min(i0 + u * BLOCK, P - 1);
+            v[u] = idx < N ? state[idx] : control[idx - N];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + u * BLOCK < P) stage[i0 + u * BLOCK] = v[u];
+    }
+    __syncthreads();
+    if (tid < L) {
+        const double* v = stage + (size_t)tid * N;
+        double x = v[0];
+        double b0[16], b1[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) b0[u] = v[min(1 + u, N - 1)];
+        for (int t0 = 1; t0 < N; t0 += 32) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) b1[u] = v[min(t0 + 16 + u, N - 1)];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (t0 + u < N) x += b0[u];
+            if (t0 + 16 >= N) break;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) b0[u] = v[min(t0 + 32 + u, N - 1)];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (t0 + 16 + u < N) x += b1[u];
+        }
+        part[tid] = x;
+    }
+    __syncthreads();
+    double s2 = 0.0;
+    if (tid == 0) {
+        s2 = part[0];
+        for (int d = 0; d < J; ++d) s2 += part[1 + d];
+        if (s2 != s2) s2 = __builtin_inf();
+    }
+    return s2;
+}
+
 // the engine runs the fused phase for J <= 16 (at most four groups of 4 joint columns)
 template <int BLOCK, bool DEFER = false>
 __device__ __forceinline__ void rollout_project(const NoiseArgs& a, int r, double* traj, double* zA, double* zB,
