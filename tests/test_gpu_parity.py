@@ -290,6 +290,16 @@ def test_golden_cfg1_optimize():
     assert st.best_cost == g["best_cost"][0]
 
 
+def test_reuse_ranking_past_the_fused_path_bitwise():
+    # K + 1 > 1024 candidates: the reuse step takes k_reuse (one workgroup per candidate, the last
+    # ranks and copies) and k_noise_rows without the fused ranking; K <= 1023 takes the fused path
+    # (the rollout launch's totals blocks, the reused rows' kernel ranks and copies)
+    p = make(K=1088, Kr=100, grid_n=64)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+
+
 @pytest.mark.parametrize("pieces", [1, 2, 3, 8, 40])
 @pytest.mark.parametrize("K,Kr,dof", [(20, 10, 7), (64, 0, 7), (16, 0, 14)])
 def test_waypoint_split_pieces_bitwise(monkeypatch, pieces, K, Kr, dof):
