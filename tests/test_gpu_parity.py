@@ -290,6 +290,17 @@ def test_golden_cfg1_optimize():
     assert st.best_cost == g["best_cost"][0]
 
 
+@pytest.mark.parametrize("waypoints,K,Kr,dof", [(200, 20, 10, 7), (30, 12, 4, 7), (200, 16, 0, 14), (12, 8, 3, 7)])
+def test_waypoint_split_shapes_bitwise(waypoints, K, Kr, dof):
+    # the split body at other shapes: N = 199 (four or more pieces: one FK wave each), a short
+    # trajectory (pieces of a few waypoints, the halo clamped at both ends), 14 DOF, with and
+    # without the fused reuse step
+    p = make(dof=dof, waypoints=waypoints, K=K, Kr=Kr, grid_n=64)
+    o, e = po.Oracle(p), eng.Engine(p)
+    for it in range(1, 5):
+        _compare_iteration(o, e, it)
+
+
 def test_reuse_ranking_past_the_fused_path_bitwise():
     # K + 1 > 1024 candidates: the reuse step takes k_reuse (one workgroup per candidate, the last
     # ranks and copies) and k_noise_rows without the fused ranking; K <= 1023 takes the fused path
