@@ -63,7 +63,7 @@ struct LocalGroup {
     // the decomposition every rank must run (gather, K, J, N), set by the first rank to join: a
     // rank that disagrees would post different collectives, so its creation fails instead
     bool has_sig = false;
-    long long sig[4] = {0, 0, 0, 0};
+    long long sig[6] = {0, 0, 0, 0, 0, 0};   // gather, K, J, N, K_r, split_modes (stomp_engine_create)
     bool broken = false;    // a rank timed out: every later barrier fails at once
     // all ranks arrive (or the wait times out: a rank not driven from a thread of its own)
     bool barrier(std::unique_lock<std::mutex>& lk)
@@ -1273,7 +1273,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || cus <= 0)
             cus = 256;
         m.cus = cus;
-        const int need = (e->K_loc + 1 + cus - 1) / cus;
+        // every workgroup of the launch counts: the rollouts, the noiseless one, the pregen blocks
+        // and the reuse candidates' totals blocks beside them (K = 448 with its 449 pregen blocks
+        // ran two workgroups per CU at 54.6 us against three at K = 512, 47.1 us: the padding
+        // positions took the slot the pregen blocks need)
+        const int blocks = e->K_loc + 1 + (e->pre_on ? e->rows : 0) + (e->Kr > 0 && world == 1 ? e->K : 0);
+        const int need = (blocks + cus - 1) / cus;
         m.pad_lds = (with_pad <= kRolloutLdsMax &&
                      rollout_blocks_per_cu(with_pad) >= std::min(need, rollout_blocks_per_cu(without))) ? 1 : 0;
         const size_t lds = rollout_lds_bytes(m, m.pad_lds) + stat;
@@ -1332,7 +1337,14 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     m.w_obs = e->w_obs; m.w_con = e->w_con; m.w_tq = e->w_tq;
     m.QT = e->d_QT;
     // piece counters of the waypoint-split rollout launches (zeroed; the last piece resets its own)
-    CREATE_TRY(dev_alloc(e, &m.split_cnt, (size_t)e->K_loc + 2));
+    // one per rollout of any split launch: split_pieces takes nro <= cus / 2 (two pieces or more
+    // per rollout), and an eval batch may hold more rows than K_loc + 1
+    m.split_cap = std::max(e->K_loc + 2, m.cus / 2 + 1);
+    CREATE_TRY(dev_alloc(e, &m.split_cnt, (size_t)m.split_cap));
+    {
+        const char* env = std::getenv("STOMP_DEBUG_SPLIT_MAX");
+        m.split_max = env ? std::atoi(env) : 0;
+    }
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);
     int pad_cf = 0;
@@ -1363,11 +1375,14 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             if (g->world != world) CREATE_TRY(fail(e, STOMP_E_COMM, "local group of %d ranks, engine world_size %d",
                                                    g->world, world));
             if (g->joined[e->rank]) CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d joined the local group twice", e->rank));
-            const long long sig[4] = {e->gather ? 1 : 0, e->K, J, N};
+            // everything that changes the per-iteration exchange sequence: the decomposition, the
+            // shapes, the reused rollouts (two more all-gathers) and the weights phases
+            const long long sig[6] = {e->gather ? 1 : 0, e->K, J, N, e->Kr, e->split_modes ? 1 : 0};
             if (g->has_sig && std::memcmp(sig, g->sig, sizeof sig) != 0)
-                CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d: decomposition (%s, K=%lld, J=%d, N=%d) differs from the group's "
-                                "(%s, K=%lld, J=%lld, N=%lld)", e->rank, e->gather ? "gather" : "partials", (long long)e->K,
-                                J, N, g->sig[0] ? "gather" : "partials", g->sig[1], g->sig[2], g->sig[3]));
+                CREATE_TRY(fail(e, STOMP_E_COMM, "rank %d: decomposition (%s, K=%lld, J=%d, N=%d, K_r=%d) differs from the "
+                                "group's (%s, K=%lld, J=%lld, N=%lld, K_r=%lld)", e->rank, e->gather ? "gather" : "partials",
+                                (long long)e->K, J, N, e->Kr, g->sig[0] ? "gather" : "partials", g->sig[1], g->sig[2],
+                                g->sig[3], g->sig[4]));
             std::memcpy(g->sig, sig, sizeof sig);
             g->has_sig = true;
             g->joined[e->rank] = 1;
@@ -1399,19 +1414,23 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         // every rank must run the same decomposition and shape, or the per-iteration collectives
         // would not pair up (one all-gather against an all-reduce and two all-gathers): one
         // all-reduce(max) of (x, -x) pairs at creation
-        const double h[8] = {e->gather ? 1.0 : 0.0, e->gather ? -1.0 : 0.0, (double)e->K, -(double)e->K,
-                             (double)J,           -(double)J,            (double)N,    -(double)N};
+        // (K_r and the weights phases too: they change the exchange sequence)
+        const double sm = e->split_modes ? 1.0 : 0.0;
+        const double h[12] = {e->gather ? 1.0 : 0.0, e->gather ? -1.0 : 0.0, (double)e->K, -(double)e->K,
+                              (double)J,           -(double)J,            (double)N,    -(double)N,
+                              (double)e->Kr,       -(double)e->Kr,        sm,           -sm};
         double* d_sig = nullptr;
-        CREATE_TRY(dev_alloc(e, &d_sig, 8));
-        double r[8];
+        CREATE_TRY(dev_alloc(e, &d_sig, 12));
+        double r[12];
         if (hipMemcpyAsync(d_sig, h, sizeof h, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
-            ncclAllReduce(d_sig, d_sig, 8, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess ||
+            ncclAllReduce(d_sig, d_sig, 12, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess ||
             hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "decomposition check across ranks failed"));
-        for (int k = 0; k < 8; k += 2)
+        for (int k = 0; k < 12; k += 2)
             if (r[k] != -r[k + 1])
-                CREATE_TRY(fail(e, STOMP_E_COMM, "ranks disagree on the K-sharded decomposition (gather, K, J, N; "
+                CREATE_TRY(fail(e, STOMP_E_COMM, "ranks disagree on the K-sharded decomposition (gather, K, J, N, K_r, "
+                                "weights phases; "
                                 "entry %d: max %g, min %g)", k / 2, r[k], -r[k + 1]));
     } else if (e->split_modes && world == 1) {
         // STOMP_DEBUG_RCCL_ONE_RANK=1 (with the sharded-modes hook): a one-rank communicator,

@@ -22,6 +22,7 @@
 // The extra workgroup (index num_noisy) evaluates the noiseless rollout of theta that the
 // previous iteration deferred (policy_improvement_loop.cpp:180-182).
 #include <algorithm>
+#include <cassert>
 #include <cstdlib>
 
 #include "device_fk.h"
@@ -103,6 +104,19 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
         v2 += c * y[kk][2];
     }
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+}
+
+// Reserve `total` (wave-uniform) entries of a block-wide LDS list for the calling wave: one LDS
+// atomic by the first active lane, its return broadcast with readlane (no lane shuffle).  The
+// pair phases build every mask of a lane's spheres first and reserve the wave's whole share at
+// once: an atomic per sphere costs three dependent LDS round trips (atomic, return, shuffle)
+// each, on the path every wave waits for at the next barrier.
+__device__ __forceinline__ int wave_reserve(int* counter, int total, int lane)
+{
+    const int leader = __ffsll((long long)__ballot(1)) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, total);
+    return __builtin_amdgcn_readlane(base, leader);
 }
 
 // max of x over the 64 lanes of the wave (every lane active): DPP within rows of 16, then
@@ -532,7 +546,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double F[12];
             int fslot = -1;
             for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
-                unsigned dv[kLaneSpheres];
+                unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
@@ -550,29 +564,44 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                         x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
                     dv[u] = sdf_d2(m, x);
                 }
+                // the thresholds read unconditionally (clamped) so the reads go out together, the
+                // a values stored after (a non-zero pair keeps its d2 until the velocity phase
+                // prices it; a = pot * |v| is +0 exactly when pot == +0)
+                unsigned nzm = 0;
+                {
+                    int2 lim[kLaneSpheres];
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        const DevSphere& sp = sph[min(pg * CPL + u0 + u, S - 1)];
+                        lim[u] = make_int2(sp.zero_lim, sp.col_lim);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        const int d2 = (int)dv[u];
+                        const bool in = (u0 + u < CPL) & (pg * CPL + u0 + u < S);
+                        col |= in & (d2 < lim[u].y);
+                        nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
+                    }
+                }
+                int total = 0;
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
                     const int sq = pg * CPL + u0 + u;
-                    const bool in = sq < S;
-                    bool nz = false;
-                    if (in) {
-                        const DevSphere& sp = sph[sq];
-                        const int d2 = (int)dv[u];
-                        col |= d2 < sp.col_lim;
-                        nz = d2 < sp.zero_lim;
-                        // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
-                        // is +0 exactly when pot == +0
-                        av[sq * N + pt] = nz ? (double)d2 : 0.0;
-                    }
-                    const unsigned long long mask = __ballot(nz);
-                    if (mask) {
-                        const int lane_id = tid & 63;
-                        const int leader = __ffsll((long long)mask) - 1;
-                        int base = 0;
-                        if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                        base = __shfl(base, leader, 64);
-                        if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(sq * N + pt);
+                    if (sq < S) av[sq * N + pt] = (nzm >> u) & 1u ? (double)dv[u] : 0.0;
+                    total += __popcll(__ballot((nzm >> u) & 1u));
+                }
+                if (total) {   // uniform: one reservation for the wave's non-zero pairs
+                    const int lane_id = tid & 63;
+                    const unsigned long long below = (1ull << lane_id) - 1ull;
+                    int off = wave_reserve(&nz_count, total, lane_id);
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        if (u0 + u >= CPL) break;   // uniform
+                        const bool nz = (nzm >> u) & 1u;
+                        const unsigned long long mk = __ballot(nz);
+                        if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg * CPL + u0 + u) * N + pt);
+                        off += __popcll(mk);
                     }
                 }
             }
@@ -640,7 +669,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // on the lanes past the pair lanes, a lookup repeats a valid one and is not used) and the
         // out-of-grid select at the use, since the compiler waits for a load whose register
         // leaves a divergent region or is copied
-        unsigned dv[kLaneSpheres];
+        unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
         unsigned okm = 0;
         {
             double F[12];
@@ -671,30 +700,50 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             __builtin_amdgcn_s_setprio(2);
         }
         if (pg < G) {
-            // the potentials and the pair list
+            // the potentials and the pair list: every sphere's mask first (bit u of nzm), then
+            // one reservation for the wave's non-zero pairs
+            // (the thresholds are read unconditionally, clamped, and no LDS store comes between
+            // them, so the reads go out together; the a values are stored after)
+            unsigned nzm = 0;
+            {
+                int2 lim[kLaneSpheres];   // (zero_lim, col_lim), every read in flight together
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    const DevSphere& sp = sph[sb + min(pg + u * G, ns - 1)];
+                    lim[u] = make_int2(sp.zero_lim, sp.col_lim);
+                }
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
+                    const bool in = pg + u * G < ns;
+                    col |= in & (d2 < lim[u].y);
+                    nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
+                }
+            }
+            int total = 0;
+#pragma unroll
+            for (int u = 0; u < kLaneSpheres; ++u) {
+                if (u * G >= ns) break;   // uniform
+                total += __popcll(__ballot((nzm >> u) & 1u));
+            }
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform
                 const int q = pg + u * G;
-                const bool in = q < ns;
-                bool nz = false;
-                if (in) {
-                    const DevSphere& sp = sph[sb + q];
-                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
-                    col |= d2 < sp.col_lim;
-                    nz = d2 < sp.zero_lim;
-                    // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
-                    // is +0 exactly when pot == +0
-                    av[q * N + pt] = nz ? (double)d2 : 0.0;
-                }
-                const unsigned long long mask = __ballot(nz);
-                if (mask) {
-                    const int lane_id = tid & 63;
-                    const int leader = __ffsll((long long)mask) - 1;
-                    int base = 0;
-                    if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                    base = __shfl(base, leader, 64);
-                    if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
+                // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
+                // is +0 exactly when pot == +0
+                if (q < ns) av[q * N + pt] = (nzm >> u) & 1u ? (double)((okm >> u) & 1u ? (int)dv[u] : 0) : 0.0;
+            }
+            if (total) {   // uniform
+                const unsigned long long below = (1ull << lane) - 1ull;
+                int off = wave_reserve(&nz_count, total, lane);
+#pragma unroll
+                for (int u = 0; u < kLaneSpheres; ++u) {
+                    if (u * G >= ns) break;   // uniform
+                    const bool nz = (nzm >> u) & 1u;
+                    const unsigned long long mk = __ballot(nz);
+                    if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg + u * G) * N + pt);
+                    off += __popcll(mk);
                 }
             }
         }
@@ -1116,7 +1165,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
             double F[12];
             int fslot = -1;
             for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
-                unsigned dv[kLaneSpheres];
+                unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
@@ -1134,25 +1183,43 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
                         x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
                     dv[u] = sdf_d2(m, x);
                 }
+                // the thresholds read unconditionally (clamped) so the reads go out together, the
+                // a values stored after (a non-zero pair keeps its d2 until the velocity phase
+                // prices it; a = pot * |v| is +0 exactly when pot == +0)
+                unsigned nzm = 0;
+                {
+                    int2 lim[kLaneSpheres];
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        const DevSphere& sp = sph[min(pg * CPL + u0 + u, S - 1)];
+                        lim[u] = make_int2(sp.zero_lim, sp.col_lim);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        const int d2 = (int)dv[u];
+                        const bool in = (u0 + u < CPL) & (pg * CPL + u0 + u < S);
+                        col |= in & (d2 < lim[u].y);
+                        nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
+                    }
+                }
+                int total = 0;
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
                     const int sq = pg * CPL + u0 + u;
-                    bool nz = false;
-                    if (sq < S) {
-                        const DevSphere& sp = sph[sq];
-                        const int d2 = (int)dv[u];
-                        col |= d2 < sp.col_lim;
-                        nz = d2 < sp.zero_lim;
-                        av[sq * Wo + pt] = nz ? (double)d2 : 0.0;
-                    }
-                    const unsigned long long mask = __ballot(nz);
-                    if (mask) {
-                        const int leader = __ffsll((long long)mask) - 1;
-                        int base = 0;
-                        if (lane == leader) base = atomicAdd(&nz_count, __popcll(mask));
-                        base = __shfl(base, leader, 64);
-                        if (nz) nzl[base + __popcll(mask & ((1ull << lane) - 1ull))] = (unsigned short)(sq * Wo + pt);
+                    if (sq < S) av[sq * Wo + pt] = (nzm >> u) & 1u ? (double)dv[u] : 0.0;
+                    total += __popcll(__ballot((nzm >> u) & 1u));
+                }
+                if (total) {   // uniform: one reservation for the wave's non-zero pairs
+                    const unsigned long long below = (1ull << lane) - 1ull;
+                    int off = wave_reserve(&nz_count, total, lane);
+#pragma unroll
+                    for (int u = 0; u < kLaneSpheres; ++u) {
+                        if (u0 + u >= CPL) break;   // uniform
+                        const bool nz = (nzm >> u) & 1u;
+                        const unsigned long long mk = __ballot(nz);
+                        if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg * CPL + u0 + u) * Wo + pt);
+                        off += __popcll(mk);
                     }
                 }
             }
@@ -1235,10 +1302,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
 // does not apply)
 int split_pieces(const DevModel& m, int nro, int pre_rows)
 {
-    if (!m.split_cnt || nro <= 0) return 0;
-    // STOMP_DEBUG_SPLIT_MAX: most pieces per rollout (1: the phased body; tests and A/B)
-    const char* env = getenv("STOMP_DEBUG_SPLIT_MAX");
-    const int cap = env ? atoi(env) : kSplitMaxDefault;
+    if (!m.split_cnt || nro <= 0 || nro > m.split_cap) return 0;   // one counter per rollout
+    // m.split_max: STOMP_DEBUG_SPLIT_MAX at creation (1: the phased body; tests and A/B)
+    const int cap = m.split_max > 0 ? m.split_max : kSplitMaxDefault;
     int P = std::min(m.cus / nro, std::min(cap, m.N));
     if (P < 2) return 0;
     // the launch's pregen blocks share it: past two workgroups per CU the split pieces take the
@@ -1361,6 +1427,7 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
     if (const int P = split_pieces(m, nro, extra_blocks)) {
         const size_t ls = rollout_split_lds_bytes(m, P);
         if (ls + 1024 <= kRolloutLdsMax) {
+            assert(nro <= m.split_cap);   // split_pieces keeps nro within the counters
             CostArgs b = a;
             b.split = P;
             b.split_cnt = m.split_cnt;

@@ -92,8 +92,12 @@ struct DevModel {
     double w_obs, w_con, w_tq;
     int pad_collision;
     const double* QT;           // [J][N][N]
-    int* split_cnt;             // [K_loc + 1] pieces done per rollout of the waypoint-split rollout
-                                // launch (zero between launches), null: no split launches
+    int* split_cnt;             // [split_cap] pieces done per rollout of the waypoint-split rollout
+                                // launch (zero between launches), null: no split launches.  Invariant:
+                                // split_cap >= the nro of every split launch (a launch's rollouts,
+                                // eval batches included); split_pieces refuses larger launches
+    int split_cap;
+    int split_max;              // most pieces per rollout (STOMP_DEBUG_SPLIT_MAX, read at creation)
 };
 
 

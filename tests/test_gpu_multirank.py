@@ -188,6 +188,20 @@ def test_ranks_disagreeing_on_the_decomposition_fail(monkeypatch):
     del e0
 
 
+def test_ranks_disagreeing_on_reused_rollouts_fail(monkeypatch):
+    # K_r changes the exchange sequence (the sharded reuse posts two more all-gathers): ranks that
+    # differ only in num_reused_rollouts are refused at creation, not left to post unmatched
+    # collectives
+    gid = eng.comm_local_id(2)
+    monkeypatch.setenv("STOMP_SHARD_MODE", "partials")
+    e0 = eng.Engine(pb.make_problem(grid_n=32, num_rollouts=128, num_reused_rollouts=0), rank=0, world_size=2,
+                    comm_id=gid)
+    with pytest.raises(RuntimeError, match="differs from the group"):
+        eng.Engine(pb.make_problem(grid_n=32, num_rollouts=128, num_reused_rollouts=64), rank=1, world_size=2,
+                   comm_id=gid)
+    del e0
+
+
 def test_cfg3_eight_rank_split_bitwise():
     # cfg3's real 8-GPU decomposition (BASELINE configs[2]): K = 4096 over 8 ranks, K_loc = 512,
     # N = 199, 256^3 device-built field, partials mode (its 6.5 MB of state rows are past gather

@@ -83,6 +83,26 @@ def test_execute_bitwise(dof):
     assert cf0 == ocf0
 
 
+def test_execute_more_rows_than_rollouts_bitwise():
+    # Task::execute batches larger than K + 1 (the facade's executeBatch with several extra
+    # rollouts): K = 20 and 40 rows run the waypoint-split launch with 40 rollouts, one piece
+    # counter each (the counters were sized K + 2); twice, so the counters' reset by the
+    # last piece is exercised too
+    p = make(K=20)
+    o, e = po.Oracle(p), eng.Engine(p)
+    rng = np.random.default_rng(11)
+    th = o.theta()
+    for rep in range(2):
+        params = th[None] + rng.standard_normal((40, p.J, p.N)).cumsum(axis=2) * 0.05
+        params[7] += 2.0   # joint limits and collisions
+        costs, cf, traj = e.execute(params, iteration_member=1)
+        for r in range(params.shape[0]):
+            oc, ocf, otr = o.execute(params[r], iteration_member=1)
+            np.testing.assert_array_equal(costs[r], oc, err_msg=f"rep {rep} row {r}")
+            np.testing.assert_array_equal(traj[r], otr)
+            assert bool(cf[r]) == ocf, (rep, r)
+
+
 def _compare_iteration(o, e, it):
     oc = o.iterate(it)
     ec = e.iterate(it)
