@@ -30,6 +30,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "stomp_engine.h"
@@ -252,6 +253,127 @@ public:
     // PolicyImprovementLoop calls; the default executes them one by one
     virtual bool executeBatch(std::vector<std::vector<VectorXd>>& parameters, std::vector<VectorXd>& costs,
                               const int iteration_number);
+};
+
+// Adapter bases for plugins written against the reference's own signatures.  The virtuals of Task
+// and Policy above take this header's VectorXd / MatrixXd; a Task or Policy written for the
+// reference overrides virtuals taking Eigen::VectorXd / Eigen::MatrixXd (task.h:62-91,
+// policy.h:59-132) and a ros::NodeHandle in Task::initialize.  Deriving such a class from
+// TaskT<Eigen::VectorXd, ros::NodeHandle> or PolicyT<Eigen::VectorXd, Eigen::MatrixXd> instead of
+// Task / Policy lets it compile unchanged: the adapters declare the reference's virtuals with those
+// types (Vector: size(), data(), resize(n); Matrix: rows(), cols(), resize(r, c), operator()(r, c);
+// NodeHandle: default-constructible, passed as a fresh object since no parameter server exists
+// here) and implement the facade's virtuals by converting and forwarding.  The policy pointers stay
+// std::shared_ptr (boost::shared_ptr in the reference, see the file header).
+template <class Vector, class NodeHandle>
+class TaskT : public Task {
+    static_assert(!std::is_same<Vector, VectorXd>::value, "TaskT<VectorXd> is Task itself");
+
+public:
+    // task.h:62 and :70 with the caller's types
+    virtual bool initialize(NodeHandle& node_handle, int num_time_steps) = 0;
+    virtual bool execute(std::vector<Vector>& parameters, Vector& costs, const int iteration_number) = 0;
+
+    bool initialize(int num_time_steps) final
+    {
+        NodeHandle nh{};
+        return initialize(nh, num_time_steps);
+    }
+    bool execute(std::vector<VectorXd>& parameters, VectorXd& costs, const int iteration_number) final
+    {
+        std::vector<Vector> p;
+        detail::from_vecs(parameters, p);
+        Vector c;
+        if (!execute(p, c, iteration_number)) return false;
+        costs = detail::to_vec(c);
+        return true;
+    }
+};
+
+template <class Vector, class Matrix>
+class PolicyT : public Policy {
+    static_assert(!std::is_same<Vector, VectorXd>::value && !std::is_same<Matrix, MatrixXd>::value,
+                  "PolicyT<VectorXd, MatrixXd> is Policy itself");
+
+public:
+    // policy.h:91-132 with the caller's types (the int-valued virtuals are Policy's own)
+    virtual bool getBasisFunctions(std::vector<Matrix>& basis_functions) = 0;
+    virtual bool getControlCosts(std::vector<Matrix>& control_costs) = 0;
+    virtual bool updateParameters(const std::vector<Matrix>& updates) = 0;
+    virtual bool getParameters(std::vector<Vector>& parameters) = 0;
+    virtual bool setParameters(const std::vector<Vector>& parameters) = 0;
+    virtual bool computeControlCosts(const std::vector<Matrix>& control_cost_matrices,
+                                     const std::vector<std::vector<Vector>>& parameters, const double weight,
+                                     std::vector<Vector>& control_costs) = 0;
+    virtual bool computeControlCosts(const std::vector<Matrix>& control_cost_matrices,
+                                     const std::vector<Vector>& parameters, const std::vector<Vector>& noise,
+                                     const double weight, std::vector<Vector>& control_costs) = 0;
+
+    bool getBasisFunctions(std::vector<MatrixXd>& basis_functions) final
+    {
+        std::vector<Matrix> b;
+        if (!getBasisFunctions(b)) return false;
+        basis_functions = mats(b);
+        return true;
+    }
+    bool getControlCosts(std::vector<MatrixXd>& control_costs) final
+    {
+        std::vector<Matrix> c;
+        if (!getControlCosts(c)) return false;
+        control_costs = mats(c);
+        return true;
+    }
+    bool updateParameters(const std::vector<MatrixXd>& updates) final { return updateParameters(unmats(updates)); }
+    bool getParameters(std::vector<VectorXd>& parameters) final
+    {
+        std::vector<Vector> p;
+        if (!getParameters(p)) return false;
+        parameters = detail::to_vecs(p);
+        return true;
+    }
+    bool setParameters(const std::vector<VectorXd>& parameters) final
+    {
+        std::vector<Vector> p;
+        detail::from_vecs(parameters, p);
+        return setParameters(p);
+    }
+    bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices,
+                             const std::vector<std::vector<VectorXd>>& parameters, const double weight,
+                             std::vector<VectorXd>& control_costs) final
+    {
+        std::vector<std::vector<Vector>> p(parameters.size());
+        for (size_t d = 0; d < parameters.size(); ++d) detail::from_vecs(parameters[d], p[d]);
+        std::vector<Vector> c;
+        if (!computeControlCosts(unmats(control_cost_matrices), p, weight, c)) return false;
+        control_costs = detail::to_vecs(c);
+        return true;
+    }
+    bool computeControlCosts(const std::vector<MatrixXd>& control_cost_matrices, const std::vector<VectorXd>& parameters,
+                             const std::vector<VectorXd>& noise, const double weight,
+                             std::vector<VectorXd>& control_costs) final
+    {
+        std::vector<Vector> p, n, c;
+        detail::from_vecs(parameters, p);
+        detail::from_vecs(noise, n);
+        if (!computeControlCosts(unmats(control_cost_matrices), p, n, weight, c)) return false;
+        control_costs = detail::to_vecs(c);
+        return true;
+    }
+
+private:
+    static std::vector<MatrixXd> mats(const std::vector<Matrix>& m)
+    {
+        std::vector<MatrixXd> o;
+        o.reserve(m.size());
+        for (const Matrix& x : m) o.push_back(detail::to_mat(x));
+        return o;
+    }
+    static std::vector<Matrix> unmats(const std::vector<MatrixXd>& m)
+    {
+        std::vector<Matrix> o(m.size());
+        for (size_t i = 0; i < m.size(); ++i) detail::from_mat(m[i], o[i]);
+        return o;
+    }
 };
 
 struct STOMPStatistics {   // msg/STOMPStatistics.msg without the ROS header

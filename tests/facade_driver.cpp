@@ -347,6 +347,127 @@ struct EigenLikeMatrix {
 };
 struct NodePlanningGroup {};
 struct NodePublisher {};
+struct NodeHandleLike {};   // ros::NodeHandle's place in Task::initialize (task.h:62)
+
+// UserPolicy written as a reference plugin: the overrides take the Eigen-shaped types of
+// policy.h:59-132 (here the stand-ins), through the PolicyT adapter
+class EigenUserPolicy : public PolicyT<EigenLikeVector, EigenLikeMatrix> {
+public:
+    EigenUserPolicy(StompOptimizer& opt, const StompTrajectory& tr, const StompParameters& q)
+        : J_(opt.numJoints()), N_(opt.numTimeSteps()), start_(tr.start), goal_(tr.goal)
+    {
+        std::shared_ptr<Policy> ctp;
+        opt.getPolicy(ctp);
+        std::vector<MatrixXd> R;
+        std::vector<VectorXd> th;
+        ok_ = ctp->getControlCosts(R) && ctp->getParameters(th);
+        R_.resize(R.size());
+        for (size_t d = 0; d < R.size(); ++d) {
+            R_[d].resize(R[d].rows(), R[d].cols());
+            R_[d].d = R[d].data_;
+        }
+        theta_.resize(th.size());
+        for (size_t d = 0; d < th.size(); ++d) theta_[d].v = th[d];
+        const int A = N_ + 12;
+        const char* names[3] = {"D0", "D1", "D2"};
+        for (int i = 0; i < 3 && ok_; ++i) {
+            D_[i].resize(A, A);
+            ok_ = stomp_engine_get_matrix(opt.engine(), names[i], 0, D_[i].d.data()) == 0;
+        }
+        w_[0] = q.smoothness_cost_velocity;
+        w_[1] = q.smoothness_cost_acceleration;
+        w_[2] = q.smoothness_cost_jerk;
+    }
+    bool ok() const { return ok_; }
+    bool setNumTimeSteps(const int n) override { return n == N_; }
+    bool getNumTimeSteps(int& n) override { n = N_; return true; }
+    bool getNumDimensions(int& d) override { d = J_; return true; }
+    bool getNumParameters(std::vector<int>& np) override { np.assign(J_, N_); return true; }
+    bool getBasisFunctions(std::vector<EigenLikeMatrix>& b) override
+    {
+        b.assign(J_, EigenLikeMatrix());
+        for (auto& m : b) {
+            m.resize(N_, N_);
+            for (int i = 0; i < N_; ++i) m(i, i) = 1.0;
+        }
+        return true;
+    }
+    bool getControlCosts(std::vector<EigenLikeMatrix>& c) override { c = R_; return true; }
+    bool updateParameters(const std::vector<EigenLikeMatrix>& u) override
+    {
+        if ((int)u.size() != J_) return false;
+        for (int d = 0; d < J_; ++d)
+            for (int t = 0; t < N_; ++t) theta_[d](t) += u[d](0, t) / 1.0;
+        return true;
+    }
+    bool getParameters(std::vector<EigenLikeVector>& p) override { p = theta_; return true; }
+    bool setParameters(const std::vector<EigenLikeVector>& p) override { theta_ = p; return true; }
+    bool computeControlCosts(const std::vector<EigenLikeMatrix>&, const std::vector<std::vector<EigenLikeVector>>&,
+                             const double, std::vector<EigenLikeVector>&) override
+    {
+        return false;   // not used by PolicyImprovement
+    }
+    bool computeControlCosts(const std::vector<EigenLikeMatrix>&, const std::vector<EigenLikeVector>& parameters,
+                             const std::vector<EigenLikeVector>& noise, const double weight,
+                             std::vector<EigenLikeVector>& costs) override
+    {
+        const int A = N_ + 12;
+        costs.assign(J_, EigenLikeVector());
+        for (int d = 0; d < J_; ++d) {
+            costs[d].resize(N_);
+            std::vector<double> x(A), all(A, 0.0);
+            for (int i = 0; i < A; ++i)
+                x[i] = i < 6 ? start_[d] : (i >= 6 + N_ ? goal_[d] : parameters[d](i - 6) + noise[d](i - 6));
+            for (int r = 0; r < 3; ++r) {
+                const double w = weight * w_[r];
+                for (int i = 0; i < A; ++i) {
+                    double acc = 0.0;
+                    for (int c = std::max(i - 3, 0); c <= std::min(i + 3, A - 1); ++c) acc += D_[r](i, c) * x[c];
+                    all[i] += w * (acc * acc);
+                }
+            }
+            for (int t = 0; t < N_; ++t) costs[d](t) = all[t + 6];
+            for (int i = 0; i < 6; ++i) {
+                costs[d](0) += all[i];
+                costs[d](N_ - 1) += all[A - (i + 1)];
+            }
+        }
+        return true;
+    }
+
+private:
+    int J_, N_;
+    VectorXd start_, goal_;
+    std::vector<EigenLikeMatrix> R_;
+    EigenLikeMatrix D_[3];
+    double w_[3];
+    std::vector<EigenLikeVector> theta_;
+    bool ok_ = false;
+};
+
+// UserTask written as a reference plugin (task.h:62-91: the node handle, Eigen-shaped execute),
+// through the TaskT adapter
+class EigenUserTask : public TaskT<EigenLikeVector, NodeHandleLike> {
+public:
+    EigenUserTask(std::shared_ptr<StompOptimizer> o, std::shared_ptr<Policy> p) : o_(std::move(o)), p_(std::move(p)) {}
+    bool initialize(NodeHandleLike& /*node_handle*/, int num_time_steps) override
+    {
+        return o_->initialize(num_time_steps);
+    }
+    bool execute(std::vector<EigenLikeVector>& parameters, EigenLikeVector& costs, const int iteration_number) override
+    {
+        ++executions;
+        return o_->execute(parameters, costs, iteration_number);   // the optimizer's Eigen-shaped overload
+    }
+    bool getPolicy(std::shared_ptr<Policy>& policy) override { policy = p_; return true; }
+    bool setPolicy(const std::shared_ptr<Policy> policy) override { p_ = policy; return true; }
+    bool getControlCostWeight(double& w) override { return o_->getControlCostWeight(w); }
+    int executions = 0;
+
+private:
+    std::shared_ptr<StompOptimizer> o_;
+    std::shared_ptr<Policy> p_;
+};
 
 int main(int argc, char** argv)
 {
@@ -569,6 +690,23 @@ int main(int argc, char** argv)
             return 24;
         }
         if (int rc = run_loop(loop, *opt, policy, out)) return rc;
+    } else if (mode == "pi_user_eigen") {
+        // pi_user with the plugins written in the reference's signatures (TaskT / PolicyT)
+        auto policy = std::make_shared<EigenUserPolicy>(*opt, p.traj, p.params);
+        if (!policy->ok()) return 50;
+        auto task = std::make_shared<EigenUserTask>(opt, policy);
+        PolicyImprovementLoop loop;
+        if (!loop.initialize(task, p.params)) {
+            std::cerr << loop.lastError() << "\n";
+            return 51;
+        }
+        if (int rc = run_loop(loop, *opt, policy, out)) return rc;
+        // every generated rollout and every noiseless rollout went through the Eigen-shaped execute
+        const int gen = p.params.num_rollouts + 9 * (p.params.num_rollouts - p.params.num_reused_rollouts);
+        if (task->executions != gen + 10) {
+            std::cerr << "executions " << task->executions << " expected " << gen + 10 << "\n";
+            return 52;
+        }
     } else if (mode == "pi_setnum") {
         // input: K_r for setNumRollouts, and 1 to initialize with the other use_cumulative_costs
         // than the optimizer's (policy_improvement.cpp:64-147): either way the rollout set stays

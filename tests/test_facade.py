@@ -188,14 +188,17 @@ def _theta_cost_rows(toks, J, N, iters, extra=0):
 
 
 @pytest.mark.gpu
-def test_facade_user_policy_matches_oracle(tmp_path):
+@pytest.mark.parametrize("mode", ["pi_user", "pi_user_eigen"])
+def test_facade_user_policy_matches_oracle(tmp_path, mode):
     # a user Policy (theta on the host) and a user Task through PolicyImprovementLoop: the host
-    # PolicyImprovement path, bit for bit the oracle's iterations (reuse included)
+    # PolicyImprovement path, bit for bit the oracle's iterations (reuse included).  pi_user_eigen:
+    # the same plugins written in the reference's own signatures (Eigen-shaped vectors and
+    # matrices, the node handle in Task::initialize) through the TaskT / PolicyT adapters
     p = pb.make_problem(grid_n=64, num_rollouts=12, num_reused_rollouts=4)
     prob, sdf = fu.write_problem(p, str(tmp_path))
     exe = fu.build_driver(str(tmp_path))
     res = str(tmp_path / "out.txt")
-    r = subprocess.run([exe, prob, sdf, "pi_user", res], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([exe, prob, sdf, mode, res], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
     rows, _ = _theta_cost_rows(open(res).read().split(), p.J, p.N, 10)
     o = po.Oracle(p)
