@@ -161,22 +161,39 @@ __device__ __forceinline__ void fk_op(const DevSegment& sg, int base, int save, 
 // (see above), and the range test moves onto the integer: round(u) in [1, n - 2].  A u below 0.5
 // truncates to 0 or below (or saturates at INT_MIN), one past the top to n - 1 or above (or
 // INT_MAX), and NaN converts to 0: every one of them fails the test, as it fails on u.
+// BRICK: the engine's 4^3 brick layout (DevModel::brick) instead of [x][y][z]; a template
+// parameter, not a branch, so the lookups stay one straight-line block
+template <bool BRICK>
 __device__ __forceinline__ unsigned sdf_cell(const DevModel& m, const double* __restrict__ p, bool& ok)
 {
     const int ix = (int)((p[0] - m.ox) * m.inv_res + 0.5);
     const int iy = (int)((p[1] - m.oy) * m.inv_res + 0.5);
     const int iz = (int)((p[2] - m.oz) * m.inv_res + 0.5);
     ok = ix >= 1 && iy >= 1 && iz >= 1 && ix <= m.nx - 2 && iy <= m.ny - 2 && iz <= m.nz - 2;
-    const unsigned cell = ((unsigned)ix * (unsigned)m.ny + (unsigned)iy) * (unsigned)m.nz + (unsigned)iz;
+    unsigned cell;
+    if constexpr (BRICK) {
+        const unsigned b = (((unsigned)ix >> 2) * (unsigned)m.nby + ((unsigned)iy >> 2)) * (unsigned)m.nbz +
+                           ((unsigned)iz >> 2);
+        cell = (b << 6) | (((unsigned)ix & 3u) << 4) | (((unsigned)iy & 3u) << 2) | ((unsigned)iz & 3u);
+    } else {
+        cell = ((unsigned)ix * (unsigned)m.ny + (unsigned)iy) * (unsigned)m.nz + (unsigned)iz;
+    }
     return ok ? cell : 0u;
 }
 
 // Returns the voxel's squared cell distance d2 (0 outside: distance 0).
+template <bool BRICK>
 __device__ __forceinline__ unsigned sdf_d2(const DevModel& m, const double* __restrict__ p)
 {
     bool ok;
-    const unsigned v = m.sdf[sdf_cell(m, p, ok)];
+    const unsigned v = m.sdf[sdf_cell<BRICK>(m, p, ok)];
     return ok ? v : 0u;
+}
+
+// the same with the layout chosen at run time (setup kernels)
+__device__ __forceinline__ unsigned sdf_d2(const DevModel& m, const double* __restrict__ p)
+{
+    return m.brick ? sdf_d2<true>(m, p) : sdf_d2<false>(m, p);
 }
 
 // PropagationDistanceField::getDistance: sqrt_table_[d2], the table made as sqrt(double(i)) * resolution

@@ -1320,6 +1320,35 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         e->d_pad_pos = (double*)(base + (L.pad - L.sph));
     }
     m.pad_pos = e->d_pad_pos; m.sdf = e->d_sdf;
+    {
+        // the field as 4^3 bricks (one 128-B line per brick) when it is large: the SDF gathers of
+        // neighbouring rollouts' spheres, which differ in x and y as much as in z, then land on
+        // shared lines (a z-fastest line holds 64 cells along z only).  STOMP_SDF_LAYOUT =
+        // brick | linear overrides.  The engine keeps its own bricked copy; the caller's field
+        // ([x][y][z], the ABI's layout) is only read here.
+        const char* lay = std::getenv("STOMP_SDF_LAYOUT");
+        const bool brick = lay ? std::strcmp(lay, "brick") == 0 : ncell * sizeof(uint16_t) > ((size_t)64 << 20);
+        m.brick = 0;
+        m.nby = (d->grid.ny + 3) / 4;
+        m.nbz = (d->grid.nz + 3) / 4;
+        if (brick) {
+            uint16_t* bricks = nullptr;
+            CREATE_TRY(dev_alloc(e, &bricks, sdf_brick_cells(d->grid.nx, d->grid.ny, d->grid.nz)));
+            launch_sdf_bricks(e->d_sdf, bricks, d->grid.nx, d->grid.ny, d->grid.nz, e->stream);
+            if (hipStreamSynchronize(e->stream) != hipSuccess)
+                CREATE_TRY(fail(e, STOMP_E_DEVICE, "distance-field brick layout failed"));
+            if (!d->grid.data_on_device) {   // the linear upload is no longer needed
+                auto it = std::find(e->allocs.begin(), e->allocs.end(), (void*)e->d_sdf);
+                if (it != e->allocs.end()) {
+                    hipFree(*it);
+                    e->allocs.erase(it);
+                }
+            }
+            e->d_sdf = bricks;
+            m.sdf = bricks;
+            m.brick = 1;
+        }
+    }
     e->terms.segs = m.segs;
     e->tq_model.segs = m.segs;
     m.nx = d->grid.nx; m.ny = d->grid.ny; m.nz = d->grid.nz;
@@ -2593,8 +2622,8 @@ int stomp_group_create(stomp_engine* const* engines, int32_t n, stomp_group** ou
         if (e->device != e0->device || e->stream != e0->stream)
             return gfail(nullptr, STOMP_E_INVALID, "the engines of a group share one device and one stream");
         if (e->J != e0->J || e->N != e0->N || e->K != e0->K || e->S != e0->S ||
-            rollout_lds_bytes(e->model, e->model.pad_lds) != lds0)
-            return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model)");
+            rollout_lds_bytes(e->model, e->model.pad_lds) != lds0 || e->model.brick != e0->model.brick)
+            return gfail(nullptr, STOMP_E_INVALID, "the engines of a group have one shape (J, N, K, spheres, model, field layout)");
         if (e->world != 1 || e->Kr != 0 || !e->pre_on || e->terms_on ||
             e->split_modes || e->gather || e->use_cum || e->J > 16)
             return gfail(nullptr, STOMP_E_UNSUPPORTED,

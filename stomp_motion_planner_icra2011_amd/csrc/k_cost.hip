@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "device_fk.h"
+#include "limits_device.h"
 #include "noise_device.h"
 #include "stamps.h"
 
@@ -106,32 +107,6 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
 }
 
-// Reserve `total` (wave-uniform) entries of a block-wide LDS list for the calling wave: one LDS
-// atomic by the first active lane, its return broadcast with readlane (no lane shuffle).  The
-// pair phases build every mask of a lane's spheres first and reserve the wave's whole share at
-// once: an atomic per sphere costs three dependent LDS round trips (atomic, return, shuffle)
-// each, on the path every wave waits for at the next barrier.
-__device__ __forceinline__ int wave_reserve(int* counter, int total, int lane)
-{
-    const int leader = __ffsll((long long)__ballot(1)) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(counter, total);
-    return __builtin_amdgcn_readlane(base, leader);
-}
-
-// max of x over the 64 lanes of the wave (every lane active): DPP within rows of 16, then
-// the four row results through scalar registers
-__device__ __forceinline__ unsigned wave_max_u32(unsigned x)
-{
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));    // quad_perm 1,0,3,2
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));    // quad_perm 2,3,0,1
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));   // row_half_mirror
-    x = max(x, (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));   // row_mirror
-    const unsigned a = __builtin_amdgcn_readlane(x, 0), b = __builtin_amdgcn_readlane(x, 16);
-    const unsigned c = __builtin_amdgcn_readlane(x, 32), d = __builtin_amdgcn_readlane(x, 48);
-    return max(max(a, b), max(c, d));
-}
-
 // handleJointLimits (stomp_optimizer.cpp:562-616) of the row in traj [J][N] (LDS) by the NW waves
 // of a workgroup; the caller publishes traj before and synchronises after.
 // Joints are independent: the limited joints are dealt round-robin over the waves and a wave
@@ -148,51 +123,13 @@ __device__ __forceinline__ void joint_limit_passes(const DevModel& m, double* tr
     // A wave keeps its joints' rows in registers through the passes (lane l: waypoints l,
     // l + 64, ...; N <= 256), so a pass is the argmax, the column load and the update with
     // no LDS round trip; the rows go back to traj after the last pass.
-    // the violated waypoint a pass corrects (wave-uniform), -1 when none is left
+    // the violated waypoint a pass corrects (wave-uniform, -1 when none is left) and the
+    // correction (limits_device.h)
     auto jl_argmax = [&](const double* v, double jmin, double jmax) -> int {
-        double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
-        int ci = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int t = lane + 64 * u;
-            if (t < N) {
-                const double x = v[u];
-                double absamt = 0.0;
-                if (x > jmax) absamt = fabs(jmax - x);
-                else if (x < jmin) absamt = fabs(jmin - x);
-                if (absamt > 1e-6 && absamt > cand) { cand = absamt; ci = t; }   // t ascending per lane
-            }
-        }
-        // wave argmax, first index on ties: the bits of a non-negative double order like
-        // the value, so the max is two 32-bit DPP reductions; ballots pick the least t
-        const unsigned long long key = (unsigned long long)__double_as_longlong(cand);
-        const unsigned hi = (unsigned)(key >> 32), lo = (unsigned)key;
-        const unsigned mh = wave_max_u32(hi);
-        const unsigned ml = wave_max_u32(hi == mh ? lo : 0u);
-        if ((mh | ml) == 0u) return -1;   // no violation left (wave-uniform)
-        const bool match = hi == mh && lo == ml;
-        int cm = 0;
-        for (int blk = 0; blk * 64 < N; ++blk) {
-            const unsigned long long b = __ballot(match && (ci >> 6) == blk);
-            if (b) { cm = blk * 64 + __ffsll((long long)b) - 1; break; }
-        }
-        return cm;
+        return stomp::jl_argmax(v, N, lane, jmin, jmax);
     };
-    // row += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606)
     auto jl_apply = [&](double* v, int cm, double jmin, double jmax, const double* qv, double qd) {
-        double vu = v[0];
-#pragma unroll
-        for (int u = 1; u < 4; ++u)
-            if ((cm >> 6) == u) vu = v[u];   // uniform select
-        const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
-        const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
-        const unsigned vhi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), cm & 63);
-        const double x = __longlong_as_double((long long)(((unsigned long long)vhi << 32) | vlo));
-        const double amount = x > jmax ? jmax - x : jmin - x;
-        const double mult = amount / qd;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (lane + 64 * u < N) v[u] += mult * qv[u];
+        stomp::jl_apply(v, N, lane, cm, jmin, jmax, qv, qd);
     };
     auto jl_pair = [&](int ja, int jb) {
         const bool hb = jb >= 0;
@@ -290,7 +227,7 @@ __device__ __forceinline__ void totals_block(const CostArgs& a, int J, int N, in
 // slot's gathers are in flight (the running frame then stays live across the pair phases); off,
 // they advance after the fold from the frame reloaded from fb (fewer live registers: the grouped
 // launch, which is throughput-bound and register-capped at three workgroups per CU)
-template <int BLOCK, bool PHASED = false, bool FK_OVERLAP = true>
+template <int BLOCK, bool BRICK, bool PHASED = false, bool FK_OVERLAP = true>
 __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -546,7 +483,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             double F[12];
             int fslot = -1;
             for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
-                unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
+                unsigned dv[kLaneSpheres];
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
@@ -562,46 +499,31 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
                     for (int i = 0; i < 3; ++i)
                         x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
-                    dv[u] = sdf_d2(m, x);
+                    dv[u] = sdf_d2<BRICK>(m, x);
                 }
-                // the thresholds read unconditionally (clamped) so the reads go out together, the
-                // a values stored after (a non-zero pair keeps its d2 until the velocity phase
-                // prices it; a = pot * |v| is +0 exactly when pot == +0)
-                unsigned nzm = 0;
-                {
-                    int2 lim[kLaneSpheres];
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        const DevSphere& sp = sph[min(pg * CPL + u0 + u, S - 1)];
-                        lim[u] = make_int2(sp.zero_lim, sp.col_lim);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        const int d2 = (int)dv[u];
-                        const bool in = (u0 + u < CPL) & (pg * CPL + u0 + u < S);
-                        col |= in & (d2 < lim[u].y);
-                        nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
-                    }
-                }
-                int total = 0;
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
                     const int sq = pg * CPL + u0 + u;
-                    if (sq < S) av[sq * N + pt] = (nzm >> u) & 1u ? (double)dv[u] : 0.0;
-                    total += __popcll(__ballot((nzm >> u) & 1u));
-                }
-                if (total) {   // uniform: one reservation for the wave's non-zero pairs
-                    const int lane_id = tid & 63;
-                    const unsigned long long below = (1ull << lane_id) - 1ull;
-                    int off = wave_reserve(&nz_count, total, lane_id);
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        if (u0 + u >= CPL) break;   // uniform
-                        const bool nz = (nzm >> u) & 1u;
-                        const unsigned long long mk = __ballot(nz);
-                        if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg * CPL + u0 + u) * N + pt);
-                        off += __popcll(mk);
+                    const bool in = sq < S;
+                    bool nz = false;
+                    if (in) {
+                        const DevSphere& sp = sph[sq];
+                        const int d2 = (int)dv[u];
+                        col |= d2 < sp.col_lim;
+                        nz = d2 < sp.zero_lim;
+                        // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
+                        // is +0 exactly when pot == +0
+                        av[sq * N + pt] = nz ? (double)d2 : 0.0;
+                    }
+                    const unsigned long long mask = __ballot(nz);
+                    if (mask) {
+                        const int lane_id = tid & 63;
+                        const int leader = __ffsll((long long)mask) - 1;
+                        int base = 0;
+                        if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                        base = __shfl(base, leader, 64);
+                        if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(sq * N + pt);
                     }
                 }
             }
@@ -669,7 +591,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // on the lanes past the pair lanes, a lookup repeats a valid one and is not used) and the
         // out-of-grid select at the use, since the compiler waits for a load whose register
         // leaves a divergent region or is copied
-        unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
+        unsigned dv[kLaneSpheres];
         unsigned okm = 0;
         {
             double F[12];
@@ -684,7 +606,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
                 for (int i = 0; i < 3; ++i)
                     x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
                 bool ok;
-                const unsigned idx = sdf_cell(m, x, ok);
+                const unsigned idx = sdf_cell<BRICK>(m, x, ok);
                 dv[u] = m.sdf[idx];
                 okm |= (unsigned)ok << u;
             }
@@ -700,50 +622,30 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             __builtin_amdgcn_s_setprio(2);
         }
         if (pg < G) {
-            // the potentials and the pair list: every sphere's mask first (bit u of nzm), then
-            // one reservation for the wave's non-zero pairs
-            // (the thresholds are read unconditionally, clamped, and no LDS store comes between
-            // them, so the reads go out together; the a values are stored after)
-            unsigned nzm = 0;
-            {
-                int2 lim[kLaneSpheres];   // (zero_lim, col_lim), every read in flight together
-#pragma unroll
-                for (int u = 0; u < kLaneSpheres; ++u) {
-                    const DevSphere& sp = sph[sb + min(pg + u * G, ns - 1)];
-                    lim[u] = make_int2(sp.zero_lim, sp.col_lim);
-                }
-#pragma unroll
-                for (int u = 0; u < kLaneSpheres; ++u) {
-                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
-                    const bool in = pg + u * G < ns;
-                    col |= in & (d2 < lim[u].y);
-                    nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
-                }
-            }
-            int total = 0;
-#pragma unroll
-            for (int u = 0; u < kLaneSpheres; ++u) {
-                if (u * G >= ns) break;   // uniform
-                total += __popcll(__ballot((nzm >> u) & 1u));
-            }
+            // the potentials and the pair list
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform
                 const int q = pg + u * G;
-                // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
-                // is +0 exactly when pot == +0
-                if (q < ns) av[q * N + pt] = (nzm >> u) & 1u ? (double)((okm >> u) & 1u ? (int)dv[u] : 0) : 0.0;
-            }
-            if (total) {   // uniform
-                const unsigned long long below = (1ull << lane) - 1ull;
-                int off = wave_reserve(&nz_count, total, lane);
-#pragma unroll
-                for (int u = 0; u < kLaneSpheres; ++u) {
-                    if (u * G >= ns) break;   // uniform
-                    const bool nz = (nzm >> u) & 1u;
-                    const unsigned long long mk = __ballot(nz);
-                    if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg + u * G) * N + pt);
-                    off += __popcll(mk);
+                const bool in = q < ns;
+                bool nz = false;
+                if (in) {
+                    const DevSphere& sp = sph[sb + q];
+                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
+                    col |= d2 < sp.col_lim;
+                    nz = d2 < sp.zero_lim;
+                    // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
+                    // is +0 exactly when pot == +0
+                    av[q * N + pt] = nz ? (double)d2 : 0.0;
+                }
+                const unsigned long long mask = __ballot(nz);
+                if (mask) {
+                    const int lane_id = tid & 63;
+                    const int leader = __ffsll((long long)mask) - 1;
+                    int base = 0;
+                    if (lane_id == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                    base = __shfl(base, leader, 64);
+                    if (nz) nzl[base + __popcll(mask & ((1ull << lane_id) - 1ull))] = (unsigned short)(q * N + pt);
                 }
             }
         }
@@ -833,23 +735,24 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     BLOCK_END();
 }
 
-template <int BLOCK>
+template <int BLOCK, bool BRICK>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
-    rollout_body<BLOCK>(m, a, blockIdx.x);
+    rollout_body<BLOCK, BRICK>(m, a, blockIdx.x);
 }
 
 // the phased evaluation for launches whose rollouts run one per CU (LDS: rollout_lds phased)
+template <bool BRICK>
 __global__ __launch_bounds__(kWideBlock, kWideBlock > 512 ? 4 : 2) void k_rollout_phased(DevModel m, CostArgs a)
 {
-    rollout_body<kWideBlock, true>(m, a, blockIdx.x);
+    rollout_body<kWideBlock, BRICK, true>(m, a, blockIdx.x);
 }
 
 // one launch for the rollouts of a group of engines of one shape (stomp_group_run): every
 // engine's rollout workgroups first (engine p's nro of them at p nro), then every engine's
 // pregen blocks (npre each, at the default priority behind them all); models and arguments
 // live in device memory, one entry per engine
-template <int BLOCK>
+template <int BLOCK, bool BRICK>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_group(const DevModel* ms, const CostArgs* as,
                                                                            int engines, int nro, int npre)
 {
@@ -863,7 +766,7 @@ __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_g
         p = j / npre;
         bid = nro + (j - p * npre);
     }
-    rollout_body<BLOCK, false, false>(ms[p], as[p], bid);
+    rollout_body<BLOCK, BRICK, false, false>(ms[p], as[p], bid);
 }
 
 // ---- the waypoint-split rollout (k_rollout_split): when a launch's rollouts fit P >= 2 to a CU
@@ -946,7 +849,7 @@ __device__ __forceinline__ double sphere_speed_w(const DevModel& m, const double
     return sqrt(v0 * v0 + v1 * v1 + v2 * v2);
 }
 
-template <int BLOCK>
+template <int BLOCK, bool BRICK>
 __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(DevModel m, CostArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -1165,7 +1068,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
             double F[12];
             int fslot = -1;
             for (int u0 = 0; u0 < CPL; u0 += kLaneSpheres) {   // uniform
-                unsigned dv[kLaneSpheres] = {};   // entries past the run stay 0 (read masked)
+                unsigned dv[kLaneSpheres];
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
@@ -1181,45 +1084,27 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
 #pragma unroll
                     for (int i = 0; i < 3; ++i)
                         x[i] = F[3 * i] * sp.pos[0] + F[3 * i + 1] * sp.pos[1] + F[3 * i + 2] * sp.pos[2] + F[9 + i];
-                    dv[u] = sdf_d2(m, x);
+                    dv[u] = sdf_d2<BRICK>(m, x);
                 }
-                // the thresholds read unconditionally (clamped) so the reads go out together, the
-                // a values stored after (a non-zero pair keeps its d2 until the velocity phase
-                // prices it; a = pot * |v| is +0 exactly when pot == +0)
-                unsigned nzm = 0;
-                {
-                    int2 lim[kLaneSpheres];
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        const DevSphere& sp = sph[min(pg * CPL + u0 + u, S - 1)];
-                        lim[u] = make_int2(sp.zero_lim, sp.col_lim);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        const int d2 = (int)dv[u];
-                        const bool in = (u0 + u < CPL) & (pg * CPL + u0 + u < S);
-                        col |= in & (d2 < lim[u].y);
-                        nzm |= (unsigned)(in & (d2 < lim[u].x)) << u;
-                    }
-                }
-                int total = 0;
 #pragma unroll
                 for (int u = 0; u < kLaneSpheres; ++u) {
                     if (u0 + u >= CPL) break;   // uniform
                     const int sq = pg * CPL + u0 + u;
-                    if (sq < S) av[sq * Wo + pt] = (nzm >> u) & 1u ? (double)dv[u] : 0.0;
-                    total += __popcll(__ballot((nzm >> u) & 1u));
-                }
-                if (total) {   // uniform: one reservation for the wave's non-zero pairs
-                    const unsigned long long below = (1ull << lane) - 1ull;
-                    int off = wave_reserve(&nz_count, total, lane);
-#pragma unroll
-                    for (int u = 0; u < kLaneSpheres; ++u) {
-                        if (u0 + u >= CPL) break;   // uniform
-                        const bool nz = (nzm >> u) & 1u;
-                        const unsigned long long mk = __ballot(nz);
-                        if (nz) nzl[off + __popcll(mk & below)] = (unsigned short)((pg * CPL + u0 + u) * Wo + pt);
-                        off += __popcll(mk);
+                    bool nz = false;
+                    if (sq < S) {
+                        const DevSphere& sp = sph[sq];
+                        const int d2 = (int)dv[u];
+                        col |= d2 < sp.col_lim;
+                        nz = d2 < sp.zero_lim;
+                        av[sq * Wo + pt] = nz ? (double)d2 : 0.0;
+                    }
+                    const unsigned long long mask = __ballot(nz);
+                    if (mask) {
+                        const int leader = __ffsll((long long)mask) - 1;
+                        int base = 0;
+                        if (lane == leader) base = atomicAdd(&nz_count, __popcll(mask));
+                        base = __shfl(base, leader, 64);
+                        if (nz) nzl[base + __popcll(mask & ((1ull << lane) - 1ull))] = (unsigned short)(sq * Wo + pt);
                     }
                 }
             }
@@ -1357,20 +1242,31 @@ void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s)
     hipLaunchKernelGGL((k_pregen<256>), dim3(rows), dim3(256), lds, s, a);
 }
 
+template <bool BRICK>
+static void launch_cost_group_t(const DevModel& m0, const DevModel* ms, const CostArgs* as, int engines, int nro,
+                                int npre, hipStream_t s)
+{
+    const int blocks = engines * (nro + npre);
+    const size_t lds = rollout_lds_bytes(m0, m0.pad_lds);
+    if (kWideBlock != kBlock && engines * nro <= m0.cus) {   // e.g. the grouped noiseless flush
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kWideBlock, BRICK>, lds);
+        hipLaunchKernelGGL((k_rollout_group<kWideBlock, BRICK>), dim3(blocks), dim3(kWideBlock), lds, s, ms, as,
+                           engines, nro, npre);
+        return;
+    }
+    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kBlock, BRICK>, lds);
+    hipLaunchKernelGGL((k_rollout_group<kBlock, BRICK>), dim3(blocks), dim3(kBlock), lds, s, ms, as, engines, nro,
+                       npre);
+}
+
 void launch_cost_group(const DevModel& m0, const DevModel* ms, const CostArgs* as, int engines, int nro, int npre,
                        hipStream_t s)
 {
-    const int blocks = engines * (nro + npre);
-    if (blocks <= 0) return;
-    const size_t lds = rollout_lds_bytes(m0, m0.pad_lds);
-    if (kWideBlock != kBlock && engines * nro <= m0.cus) {   // e.g. the grouped noiseless flush
-        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kWideBlock>, lds);
-        hipLaunchKernelGGL((k_rollout_group<kWideBlock>), dim3(blocks), dim3(kWideBlock), lds, s, ms, as, engines, nro,
-                           npre);
-        return;
-    }
-    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout_group<kBlock>, lds);
-    hipLaunchKernelGGL((k_rollout_group<kBlock>), dim3(blocks), dim3(kBlock), lds, s, ms, as, engines, nro, npre);
+    if (engines * (nro + npre) <= 0) return;
+    // the group's engines share one shape; the layout is each engine's (its own field copy when
+    // bricked), and one launch takes one layout: the group is made of engines of one layout
+    if (m0.brick) launch_cost_group_t<true>(m0, ms, as, engines, nro, npre, s);
+    else launch_cost_group_t<false>(m0, ms, as, engines, nro, npre, s);
 }
 
 bool cost_supported(const DevModel& m)
@@ -1388,7 +1284,7 @@ size_t rollout_phased_lds_bytes(const DevModel& m)
     const size_t dyn = rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds, true).total;
     hipFuncAttributes attr;
     size_t stat = 2048;
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout_phased) == hipSuccess) stat = attr.sharedSizeBytes;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout_phased<false>) == hipSuccess) stat = attr.sharedSizeBytes;
     if ((size_t)m.S * m.N > 65535 || dyn + stat > kLdsPerCu) return 0;   // pair ids are 16-bit
     return dyn;
 }
@@ -1396,7 +1292,7 @@ size_t rollout_phased_lds_bytes(const DevModel& m)
 size_t rollout_static_lds()
 {
     hipFuncAttributes attr;
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock>) != hipSuccess) return 2048;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false>) != hipSuccess) return 2048;
     return attr.sharedSizeBytes;
 }
 
@@ -1407,7 +1303,7 @@ int rollout_blocks_per_cu(size_t lds_total)
 {
     hipFuncAttributes attr;
     int regs = 256;
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock>) == hipSuccess && attr.numRegs > 0)
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false>) == hipSuccess && attr.numRegs > 0)
         regs = attr.numRegs;
     const int alloc = (regs + 7) / 8 * 8;
     int waves_per_simd = 512 / alloc;
@@ -1417,12 +1313,12 @@ int rollout_blocks_per_cu(size_t lds_total)
     return by_regs < by_lds ? by_regs : by_lds;
 }
 
-void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
+template <bool BRICK>
+static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int nro = a.num_noisy + (a.x_params ? 1 : 0);
     const int extra_blocks = (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows;   // pregen, then totals
     const int blocks = nro + extra_blocks;
-    if (blocks <= 0) return;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
     if (const int P = split_pieces(m, nro, extra_blocks)) {
         const size_t ls = rollout_split_lds_bytes(m, P);
@@ -1431,25 +1327,32 @@ void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
             CostArgs b = a;
             b.split = P;
             b.split_cnt = m.split_cnt;
-            lds_opt_in((const void*)k_rollout_split<kSplitBlock>, ls);
-            hipLaunchKernelGGL((k_rollout_split<kSplitBlock>), dim3(nro * P + extra_blocks), dim3(kSplitBlock), ls, s, m,
-                               b);
+            lds_opt_in((const void*)k_rollout_split<kSplitBlock, BRICK>, ls);
+            hipLaunchKernelGGL((k_rollout_split<kSplitBlock, BRICK>), dim3(nro * P + extra_blocks), dim3(kSplitBlock),
+                               ls, s, m, b);
             return;
         }
     }
     if (kWideBlock != kBlock && nro <= m.cus && m.phased_lds > 0) {
         const size_t lp = m.phased_lds;
-        lds_opt_in((const void*)k_rollout_phased, lp);
-        hipLaunchKernelGGL(k_rollout_phased, dim3(blocks), dim3(kWideBlock), lp, s, m, a);
+        lds_opt_in((const void*)k_rollout_phased<BRICK>, lp);
+        hipLaunchKernelGGL(k_rollout_phased<BRICK>, dim3(blocks), dim3(kWideBlock), lp, s, m, a);
         return;
     }
     if (kWideBlock != kBlock && nro <= m.cus) {
-        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock>, lds);
-        hipLaunchKernelGGL((k_rollout<kWideBlock>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);
+        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock, BRICK>, lds);
+        hipLaunchKernelGGL((k_rollout<kWideBlock, BRICK>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);
         return;
     }
-    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock>, lds);
-    hipLaunchKernelGGL((k_rollout<kBlock>), dim3(blocks), dim3(kBlock), lds, s, m, a);
+    if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK>, lds);
+    hipLaunchKernelGGL((k_rollout<kBlock, BRICK>), dim3(blocks), dim3(kBlock), lds, s, m, a);
+}
+
+void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
+{
+    if (a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows <= 0) return;
+    if (m.brick) launch_cost_t<true>(m, a, s);
+    else launch_cost_t<false>(m, a, s);
 }
 
 }  // namespace stomp

@@ -15,6 +15,8 @@
 //                   min(d2, cap^2), the field's squared cell distance (distance = sqrt(d2) * res)
 // oracle/sdf_oracle.c restates the same rules (with a sweep for the z pass); the tests compare the
 // fields bit for bit.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace stomp {
@@ -152,6 +154,28 @@ __global__ __launch_bounds__(256) void k_edt_window(int nx, int ny, int nz, int 
         }
     }
     out[idx] = (unsigned short)(FINAL && best > far - 1 ? far - 1 : best);   // the last pass: min(d2, cap^2)
+}
+
+// [nx][ny][nz] -> 4^3 bricks (kernels.h DevModel::brick): one lane per destination voxel, so the
+// stores are coalesced and each brick's 64 reads come from 16 z-runs of 4
+__global__ __launch_bounds__(256) void k_sdf_bricks(const unsigned short* src, unsigned short* dst, int nx, int ny,
+                                                    int nz, size_t total)
+{
+    const int nby = (ny + 3) / 4, nbz = (nz + 3) / 4;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t b = i >> 6;
+        const int in = (int)(i & 63);
+        const int bz = (int)(b % nbz), by = (int)((b / nbz) % nby), bx = (int)(b / ((size_t)nbz * nby));
+        const int x = 4 * bx + (in >> 4), y = 4 * by + ((in >> 2) & 3), z = 4 * bz + (in & 3);
+        dst[i] = (x < nx && y < ny && z < nz) ? src[((size_t)x * ny + y) * nz + z] : (unsigned short)0;
+    }
+}
+
+void launch_sdf_bricks(const unsigned short* src, unsigned short* dst, int nx, int ny, int nz, hipStream_t s)
+{
+    const size_t total = sdf_brick_cells(nx, ny, nz);
+    const size_t blocks = std::min<size_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_sdf_bricks, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, nx, ny, nz, total);
 }
 
 void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMarkArgs& g, hipStream_t s)

@@ -81,8 +81,12 @@ struct DevModel {
     const FkOp* ops;
     const int* slot_sph;        // [nslots+1] spheres of slot g: [slot_sph[g], slot_sph[g+1])
     const double* pad_pos;      // [12][S][3]
-    const unsigned short* sdf;  // d2 per voxel
+    const unsigned short* sdf;  // d2 per voxel: [nx][ny][nz] (z fastest), or 4x4x4 bricks (brick)
     int nx, ny, nz;
+    int brick;                  // bricks of 4^3 voxels (128 B, one L2 line): brick (bx, by, bz) at
+                                // ((bx nby + by) nbz + bz) 64, voxel (x, y, z) & 3 inside at
+                                // (x & 3) 16 + (y & 3) 4 + (z & 3)
+    int nby, nbz;               // bricks per y / z axis (ceil(n / 4))
     double ox, oy, oz, res, inv_res;
     double ny_d, nz_d;          // ny, nz as doubles (the fp64 cell index of sdf_d2)
     double hi_x, hi_y, hi_z;    // n - 1.5 per axis: round(u) <= n - 2 <=> u < n - 1.5
@@ -421,5 +425,12 @@ void launch_mark_lattice(const SdfLatticeJob& j, const double* axes, const SdfMa
 void launch_mark_points(const double* pts, long long np, const SdfMarkArgs& g, hipStream_t s);
 void launch_edt(int nx, int ny, int nz, int cap, const unsigned char* occ, unsigned short* a, unsigned short* b,
                 unsigned short* field, hipStream_t s);
+// the [nx][ny][nz] field re-laid as 4^3 bricks (DevModel::brick) into dst, ceil(n / 4)^3 bricks;
+// voxels of the padding bricks past the grid are 0 (never read: the lookup's range test)
+void launch_sdf_bricks(const unsigned short* src, unsigned short* dst, int nx, int ny, int nz, hipStream_t s);
+inline size_t sdf_brick_cells(int nx, int ny, int nz)
+{
+    return (size_t)((nx + 3) / 4) * ((ny + 3) / 4) * ((nz + 3) / 4) * 64;
+}
 
 }  // namespace stomp

@@ -103,6 +103,25 @@ def test_execute_more_rows_than_rollouts_bitwise():
             assert bool(cf[r]) == ocf, (rep, r)
 
 
+@pytest.mark.parametrize("grid_n,K", [(64, 20), (66, 10)])
+def test_brick_layout_bitwise(monkeypatch, grid_n, K):
+    # the distance field re-laid as 4^3 bricks inside the engine (the default past 64 MiB, 512^3):
+    # same voxels, same lookups, so every iteration is bit-identical; 66 is not a multiple of 4
+    # (padding bricks)
+    monkeypatch.setenv("STOMP_SDF_LAYOUT", "brick")
+    p = make(K=K, grid_n=grid_n)
+    o, e = po.Oracle(p), eng.Engine(p)
+    for it in range(1, 6):
+        _compare_iteration(o, e, it)
+    rng = np.random.default_rng(5)
+    params = o.theta()[None] + rng.standard_normal((4, p.J, p.N)).cumsum(axis=2) * 0.08
+    costs, cf, _ = e.execute(params, iteration_member=1)
+    for r in range(4):
+        oc, ocf, _ = o.execute(params[r], iteration_member=1)
+        np.testing.assert_array_equal(costs[r], oc)
+        assert bool(cf[r]) == ocf
+
+
 def _compare_iteration(o, e, it):
     oc = o.iterate(it)
     ec = e.iterate(it)
