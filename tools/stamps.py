@@ -131,4 +131,49 @@ def residency():
           f"{int((t1 - t0).min())}/{int(np.median(t1 - t0))}/{int((t1 - t0).max())}")
 
 
+
+def slowest_detail(it=9, count=3):
+    """Phase stamps of the slowest rollout workgroups of one launch (and the fastest): the
+    residency record of iteration it picks them, then theta is restored and the same iteration is
+    run again with the stamps on each picked block (the noise is counter-based, so block b is the
+    same rollout both times)."""
+    fn = lib.stomp_debug_blocks_cost
+    fn.argtypes = [C.c_void_p]
+    th = e.theta()
+    e.run(it, 1)
+    e.synchronize()
+    buf = np.zeros((8192, 6), np.uint64)
+    fn(buf.ctypes.data)
+    b = buf[:K].astype(np.int64)
+    dur = b[:, 3] - b[:, 2]
+    order = np.argsort(-dur)
+    print(f"--- iteration {it}: rollout WG duration min/median/max {int(dur.min())}/{int(np.median(dur))}/{int(dur.max())}")
+    picks = [int(i) for i in order[:count]] + [int(order[-1])]
+    for blk in picks:
+        e.set_theta(th)
+        show_one(blk, it, int(dur[blk]))
+
+
+def show_one(block, it, dur):
+    fn = lib.stomp_debug_stamps_cost
+    fn.argtypes = [C.c_int, C.c_void_p, C.c_int]
+    fn(block, None, 1)
+    e.run(it, 1)
+    e.synchronize()
+    fn(block, buf, 0)
+    v = np.array(buf[:], dtype=np.int64)
+    idx = sorted([i for i in range(256) if v[i] != 0], key=lambda i: v[i])
+    if not idx:
+        print("no stamps")
+        return
+    t0 = v[idx[0]]
+    print(f"--- block {block} (residency-pass duration {dur}): total {v[idx[-1]] - t0} cycles")
+    prev = t0
+    for i in idx:
+        print(f"  {cost_label(i):28s} +{v[i] - prev:8d}  @{v[i] - t0:8d}")
+        prev = v[i]
+
+
 residency()
+if os.environ.get("STAMP_SLOW"):
+    slowest_detail()
