@@ -18,7 +18,7 @@ BUILD = os.path.join(ROOT, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["k_noise.hip", "k_cost.hip", "k_terms.hip", "k_weights.hip", "k_misc.hip", "k_sdf.hip", "selftest.hip", "engine.cpp", "setup.cpp"]
-HEADERS = ["kernels.h", "setup.h", "stomp_math.h", "device_fk.h", "stamps.h", "noise_device.h", "limits_device.h"]
+HEADERS = ["kernels.h", "setup.h", "stomp_math.h", "device_fk.h", "stamps.h", "noise_device.h", "limits_device.h", "update_device.h"]
 
 # One rounding per operation on host and device (parity with the oracle's FP contract).
 COMMON = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-Wall",

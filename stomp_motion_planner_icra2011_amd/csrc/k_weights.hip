@@ -12,6 +12,7 @@
 // the K-sharded multi-GPU result bit-identical to one GPU: the W_MINMAX / W_PSUM / W_USUM
 // phases emit exactly the per-block partials the fused mode sums, and RCCL moves them.
 #include "kernels.h"
+#include "update_device.h"
 #include "noise_device.h"
 #include "stomp_math.h"
 #include "stamps.h"
@@ -563,74 +564,19 @@ __device__ __forceinline__ void update_body(int d, int J, int N, const double* M
     else theta[(size_t)d * N + i] += 1.0 * s;
 }
 
-// One WG per (16 outputs, joint), 7 x 7 = 49 WGs at cfg2: the tile's columns of every M^T row
-// are staged in LDS with all the loads in flight at once (M's rows come from HBM after the
-// rollout launch; the ring of update_body, which k_update_group keeps, waits on them ~8 times),
-// then 16 lanes run the k-ascending chain out of LDS (same products, same order, one rounding per
-// multiply and per add, exactly N terms).  LDS: 17 N doubles.  Measured: rocprof 4.75 -> 4.57 us;
-// 64-column tiles 5.78 us, 8 columns and LDS reads one batch ahead no better (profiles/ab/r3_update_tiles.txt).
-#ifndef UPDATE_COLS
-#define UPDATE_COLS 16
-#endif
-constexpr int kUpdCols = UPDATE_COLS;
-constexpr int kUpdLoads = (128 * kUpdCols + 255) / 256;   // 8-byte loads per lane per batch (one batch while N <= 128)
-
+// One WG per (16 outputs, joint), 7 x 7 = 49 WGs at cfg2 (update_tile, update_device.h): the tile's
+// columns of every M^T row are staged in LDS with all the loads in flight at once (M's rows come
+// from HBM after the rollout launch; the ring of update_body, which k_update_group keeps, waits on
+// them ~8 times), then 16 lanes run the k-ascending chain out of LDS.  LDS: 17 N doubles.
+// Measured: rocprof 4.75 -> 4.57 us; 64-column tiles 5.78 us, 8 columns and LDS reads one batch
+// ahead no better (profiles/ab/r3_update_tiles.txt).
 __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, const double* u, const double* u_all,
                                                 int nb_total, double* theta, const int* stop, double* delta)
 {
-    extern __shared__ double ms[];   // [N][kUpdCols], then us[N]
-    double* us = ms + (size_t)N * kUpdCols;
-    const int tid = threadIdx.x;
-    const int c0 = blockIdx.x * kUpdCols, d = blockIdx.y;
-    const int nc = min(kUpdCols, N - c0);
+    extern __shared__ double ms[];   // [N][kUpdCols], then u[N]
     const int stopped = stop ? *stop : 0;
-    const size_t JN = (size_t)J * N;
-    const int total = N * kUpdCols;
-    for (int f0 = 0; f0 < total; f0 += kUpdLoads * 256) {
-        double v[kUpdLoads];
-#pragma unroll
-        for (int q = 0; q < kUpdLoads; ++q) {
-            // clamped addresses: every lane loads, the stores below keep the rows that exist
-            const int f = f0 + tid + q * 256;
-            const int k = min(f / kUpdCols, N - 1), c = min(f % kUpdCols, nc - 1);
-            v[q] = MT[(size_t)k * N + c0 + c];
-        }
-        if (tid < N) {
-            double uv = 0.0;
-            if (f0 == 0) {
-                if (u_all) {
-                    for (int b = 0; b < nb_total; ++b) uv += u_all[(size_t)b * JN + (size_t)d * N + tid];
-                } else {
-                    uv = u[(size_t)d * N + tid];
-                }
-                us[tid] = uv;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kUpdLoads; ++q) {
-            const int f = f0 + tid + q * 256;
-            if (f < total) ms[f] = v[q];
-        }
-    }
-    __syncthreads();
-    if (tid >= kUpdCols) return;
-    double s = 0.0;
-    int k = 0;
-    for (; k + 8 <= N; k += 8) {
-        double a[8], x[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            a[q] = ms[(k + q) * kUpdCols + tid];
-            x[q] = us[k + q];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s += a[q] * x[q];
-    }
-    for (; k < N; ++k) s += ms[k * kUpdCols + tid] * us[k];
-    if (tid >= nc || stopped) return;
-    const int i = c0 + tid;
-    if (delta) delta[(size_t)d * N + i] = s;   // improvePolicy's update alone (PolicyImprovement API)
-    else theta[(size_t)d * N + i] += 1.0 * s;
+    update_tile(J, N, MT, u, u_all, nb_total, theta, stopped != 0, delta, blockIdx.x * kUpdCols, blockIdx.y, ms,
+                threadIdx.x);
 }
 
 // the updates of a group of engines in one launch (engine p's joint d at p J + d)
@@ -675,7 +621,7 @@ void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,
                    const int* stop, hipStream_t s, double* delta)
 {
-    const size_t lds = ((size_t)N * kUpdCols + N) * sizeof(double);
+    const size_t lds = update_tile_lds_bytes(N);
     if (lds > 48 * 1024) lds_opt_in((const void*)k_update, lds);
     hipLaunchKernelGGL(k_update, dim3((N + kUpdCols - 1) / kUpdCols, J), dim3(256), lds, s, J, N, MT, u, u_all,
                        nb_total, theta, stop, delta);

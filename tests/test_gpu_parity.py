@@ -122,6 +122,39 @@ def test_brick_layout_bitwise(monkeypatch, grid_n, K):
         assert bool(cf[r]) == ocf
 
 
+def test_slot_loop_runs_between_other_calls_bitwise():
+    # K + 1 > CUs (the slot-loop launches of cfg2), pipelined runs interleaved with get_theta,
+    # iterate, execute and set_theta: the pending noiseless rollout and the pregen rows made ahead
+    # stay consistent across the calls
+    p = make(K=320, grid_n=64)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    e.run(1, 4)
+    for it in range(1, 5):
+        o.iterate(it)
+    np.testing.assert_array_equal(e.theta(), o.theta())          # get_theta flushes
+    e.run(5, 3)
+    for it in range(5, 8):
+        o.iterate(it)
+    _compare_iteration(o, e, 8)                                     # iterate after a run
+    e.run(9, 2)
+    e.synchronize()
+    for it in range(9, 11):
+        o.iterate(it)
+    costs, cf, _ = e.execute(o.theta()[None], iteration_member=1)   # execute after a run
+    oc, ocf, _ = o.execute(o.theta(), iteration_member=1)
+    np.testing.assert_array_equal(costs[0], oc)
+    np.testing.assert_array_equal(e.last_trajectory(), o.last_trajectory())
+    th = o.theta() + 0.01
+    e.set_theta(th)
+    o.set_theta(th)
+    e.run(11, 3)
+    for it in range(11, 14):
+        o.iterate(it)
+    np.testing.assert_array_equal(e.theta(), o.theta())
+    for f in ("state_costs", "probabilities"):
+        np.testing.assert_array_equal(e.rollouts(f), o.rollouts(f), err_msg=f)
+
+
 def _compare_iteration(o, e, it):
     oc = o.iterate(it)
     ec = e.iterate(it)
