@@ -258,6 +258,17 @@ def cpu_baseline_all_cores(problem, budget_s: float):
                       f"{h['sched_affinity']} CPUs), {el:.1f} s"}
 
 
+def shard_why(e) -> str:
+    """why the engine chose its K-sharded decomposition (measured at creation, maxima over ranks)"""
+    i = e.shard_info
+    if not i:
+        return ""
+    g = i["t_gather"] + i["l_allgather_state"]
+    p = i["t_partials"] + i["l_allreduce"] + 2 * i["l_allgather_partials"]
+    return (f": measured gather {i['t_gather']:.1f} + all-gather {i['l_allgather_state']:.1f} = {g:.1f} us vs "
+            f"partials {i['t_partials']:.1f} + 3 collectives {p - i['t_partials']:.1f} = {p:.1f} us")
+
+
 def max_over_ranks(dist, x: float) -> float:
     if not dist:
         return x
@@ -551,8 +562,9 @@ def main():
             "config": {"workload": f"{workload_name(args)}: {args.dof}-DOF, {args.waypoints} wp (N={p.N}), K={K} "
                                    f"({K_loc}/GPU), K_r={args.reused}, {args.grid}^3 SDF, S={S} spheres",
                        "global_rollouts": K, "rollouts_per_gpu": K_loc,
-                       "parallelism": f"rollout shard x{world}" + (f" (RCCL, {e.shard_mode})"
+                       "parallelism": f"rollout shard x{world}" + (f" (RCCL, {e.shard_mode}{shard_why(e)})"
                                                                      if world > 1 else ""),
+                       "shard_choice": e.shard_info,
                        "rollouts_per_s": round(value * K, 1)},
             "roofline": roofline,
             "cpu_baseline": cpu,

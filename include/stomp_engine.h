@@ -265,6 +265,16 @@ int stomp_engine_local_rollouts(stomp_engine* e, int32_t* first, int32_t* count)
 #define STOMP_SHARD_PARTIALS 1
 #define STOMP_SHARD_GATHER 2
 int stomp_engine_shard_mode(stomp_engine* e, int32_t* mode);
+/* How the decomposition was chosen.  info[0] = the mode; when both were possible and none was
+ * requested (STOMP_SHARD_MODE unset, world > 1) the engine measured at creation, maxima over the
+ * ranks, in microseconds: info[1] = one iteration's compute in gather mode, info[2] = in partials mode
+ * (no exchanges), info[3] = the all-reduce(max) of 2 J N doubles, info[4] = the all-gather of the
+ * state-cost rows, info[5] = the all-gather of the block partials; zeros otherwise. */
+int stomp_engine_shard_info(stomp_engine* e, double* info);
+/* The rule applied to those measurements (host only): gather when info[1] + info[4] <=
+ * info[2] + info[3] + 2 info[5] (one all-gather against three dependent collectives).
+ * measured = info + 1. */
+int stomp_shard_decide(const double* measured, int32_t* mode);
 
 /* Distance-field builder (capped exact EDT, stomp_grid's representation):
  *   value = min(d2, ceil(max_expansion/res)^2)   (the cap must be <= 255 cells)

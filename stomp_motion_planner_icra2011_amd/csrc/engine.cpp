@@ -104,6 +104,12 @@ struct stomp_engine {
     // rows per iteration gives every rank the whole cost matrix for the fused weights and the update
     bool gather = false;
     int rows = 0, row0 = 0;   // rollout rows held per iteration (K_loc, or K in gather mode); own rows' offset
+    // the decomposition measured at creation (calibrate_shard_mode): both are possible and none was
+    // requested, so the buffers hold all K rows and the ranks time each decomposition's compute and
+    // collectives, then pick the faster.  shard_info: mode, T_gather, T_partials (us per iteration
+    // without exchanges), L_allreduce, L_allgather_state, L_allgather_partials (us per collective)
+    bool calibrate = false;
+    double shard_info[6] = {0, 0, 0, 0, 0, 0};
     uint64_t seed = 0;
     double disc = 0.05, w_smooth = 0, w_obs = 0, w_con = 0, w_tq = 0;
     double smooth[3] = {0, 0, 0};
@@ -855,6 +861,128 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     return 0;
 }
 
+// The K-sharded decomposition from measurements, at the end of stomp_engine_create when
+// both are possible and none was requested.  Every rank times, on its own device and stream:
+//   T_g  one iteration's rollout launch and fused weights in gather mode (its K_loc rollouts, all K
+//        pregen / pricing rows, the weights over all K), no exchange;
+//   T_p  the same in partials mode (its K_loc rows, the MINMAX / PSUM / USUM weights phases);
+//   L_ar, L_ag, L_agp  the collectives each posts: the all-reduce(max) of 2 J N doubles, the
+//        all-gather of the K_loc N state rows, the all-gather of the block partials;
+// the maxima over the ranks are taken (one all-reduce), so every rank decides alike:
+//   gather  <=>  T_g + L_ag <= T_p + L_ar + 2 L_agp          (stomp_shard_decide)
+// The calibration launches leave no state the first iteration reads: theta is untouched, the pregen
+// rows are remade (pre_it stays -1), and every row buffer is rewritten by the iterations.
+// STOMP_DEBUG_SHARD_LATENCY_US=x adds x us to every measured collective (tests: both selections).
+int calibrate_shard_mode(stomp_engine* e)
+{
+    const int J = e->J, N = e->N;
+    const size_t JN = (size_t)J * N;
+    hipEvent_t ev0 = get_event(e), ev1 = get_event(e);
+    auto elapsed_us = [&]() -> double {
+        float ms = 0.0f;
+        if (hipEventSynchronize(ev1) != hipSuccess || hipEventElapsedTime(&ms, ev0, ev1) != hipSuccess) return -1.0;
+        return 1000.0 * ms;
+    };
+    auto median = [](std::vector<double> v) {
+        std::sort(v.begin(), v.end());
+        return v[v.size() / 2];
+    };
+    auto set_mode = [&](bool gather) {
+        e->gather = gather;
+        e->rows = gather ? e->K : e->K_loc;
+        e->row0 = gather ? e->first : 0;
+        e->split_modes = !gather;
+    };
+    // one iteration's compute in the current mode (enqueue_iteration's launches for K_r = 0 with
+    // pregen rows, the exchanges left out)
+    auto compute = [&]() -> double {
+        NoiseArgs na = noise_args(e, 1);
+        na.K_gen_global = e->K;
+        na.row_begin = e->rows;
+        na.rows_in_pre = 1;
+        CostArgs ca{};
+        ca.stop = e->d_stop;
+        ca.fused_noise = 2;
+        ca.nz = na;
+        ca.params = e->d_params; ca.stride = (long long)JN; ca.num_noisy = e->K_loc;
+        ca.member = 0;
+        ca.pre_rows = e->rows;
+        ca.pre_next = pregen_args(e, 2);
+        ca.ctl_by_pre = 1;
+        ca.ctl_rows = e->rows;
+        ca.row0 = e->row0;
+        ca.state_out = e->d_state + (size_t)e->row0 * N;
+        WeightArgs wa{};
+        wa.stop = e->d_stop;
+        wa.J = J; wa.N = N; wa.K_loc = e->rows; wa.use_cumulative = e->use_cum;
+        wa.state = e->d_state; wa.control = e->d_control; wa.noise = na.pre_eps;
+        wa.cum = e->use_cum ? e->d_cum : nullptr; wa.prob = e->d_prob; wa.u = e->d_u;
+        wa.tc = weights_tile(e->rows);
+        wa.nb_total = e->K / kSumBlock;
+        wa.mm = e->d_mm; wa.psum_part = e->d_psum_part; wa.psum_all = e->d_psum_all; wa.u_part = e->d_u_part;
+        hipEventRecord(ev0, e->stream);
+        launch_cost(e->model, ca, e->stream);
+        if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
+        if (!e->split_modes) {
+            wa.mode = W_FUSED;
+            launch_weights(wa, e->stream);
+        } else {
+            for (int mode : {W_MINMAX, W_PSUM, W_USUM}) {
+                wa.mode = mode;
+                launch_weights(wa, e->stream);
+            }
+        }
+        hipEventRecord(ev1, e->stream);
+        return elapsed_us();
+    };
+    auto timed = [&](auto&& f, int reps) -> double {
+        f();   // warm
+        std::vector<double> v;
+        for (int r = 0; r < reps; ++r) v.push_back(f());
+        return median(v);
+    };
+    double m[5];
+    set_mode(true);
+    m[0] = timed(compute, 3);
+    set_mode(false);
+    m[1] = timed(compute, 3);
+    int rc = 0;
+    auto coll = [&](auto&& post) -> double {
+        hipEventRecord(ev0, e->stream);
+        if (int r = post()) rc = r;
+        hipEventRecord(ev1, e->stream);
+        return elapsed_us();
+    };
+    m[2] = timed([&]() { return coll([&]() { return exchange_max(e, e->d_mm, 2 * JN); }); }, 8);
+    m[3] = timed([&]() {
+        return coll([&]() { return exchange_gather(e, e->d_state + (size_t)e->first * N, e->d_state,
+                                                   (size_t)e->K_loc * N); });
+    }, 8);
+    m[4] = timed([&]() {
+        return coll([&]() { return exchange_gather(e, e->d_psum_part, e->d_psum_all,
+                                                   (size_t)(e->K_loc / kSumBlock) * JN); });
+    }, 8);
+    e->pool.push_back(ev0);
+    e->pool.push_back(ev1);
+    if (rc) return rc;
+    for (double x : m)
+        if (!(x >= 0.0)) return fail(e, STOMP_E_DEVICE, "decomposition calibration: event timing failed");
+    if (const char* lat = std::getenv("STOMP_DEBUG_SHARD_LATENCY_US"))
+        for (int k = 2; k < 5; ++k) m[k] += std::atof(lat);
+    // every rank decides on the maxima over the ranks
+    HIP_TRY(e, hipMemcpyAsync(e->d_mm, m, sizeof m, hipMemcpyHostToDevice, e->stream));
+    if ((rc = exchange_max(e, e->d_mm, 5))) return rc;
+    HIP_TRY(e, hipMemcpyAsync(m, e->d_mm, sizeof m, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    int32_t mode = 0;
+    stomp_shard_decide(m, &mode);
+    set_mode(mode == STOMP_SHARD_GATHER);
+    if (e->gather) HIP_TRY(e, hipMemsetAsync(e->d_state, 0, sizeof(double) * e->rows * N, e->stream));
+    e->shard_info[0] = mode;
+    for (int k = 0; k < 5; ++k) e->shard_info[1 + k] = m[k];
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -994,6 +1122,14 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         } else if (world > 1 && can) {
             e->gather = sm ? std::strcmp(sm, "gather") == 0 : (size_t)e->K * e->N * sizeof(double) <= (1u << 20);
         }
+        // with both decompositions possible and none requested, the choice is measured at the end of
+        // creation (calibrate_shard_mode); until then gather mode's layout, which holds every row
+        // (the in-process exchange group calibrates only on request, STOMP_DEBUG_CALIBRATE_LOCAL=1:
+        // its ranks must then be created on host threads of their own, as the measurement exchanges)
+        const char* cl = std::getenv("STOMP_DEBUG_CALIBRATE_LOCAL");
+        const bool local = world > 1 && std::memcmp(d->comm_id, kLocalMagic, sizeof kLocalMagic) == 0;
+        e->calibrate = world > 1 && can && !sm && (!local || (cl && cl[0] == '1'));
+        if (e->calibrate) e->gather = true;
         e->rows = e->gather ? e->K : e->K_loc;
         e->row0 = (e->gather && world > 1) ? e->first : 0;
         // STOMP_DEBUG_SHARDED_MODES=1: a one-device engine runs the multi-GPU weights phases
@@ -1109,7 +1245,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
     if (e->use_cum) CREATE_TRY(dev_alloc(e, &e->d_cum, KJN));
     CREATE_TRY(dev_alloc(e, &e->d_u, (size_t)J * N));
-    if (e->split_modes) {
+    if (e->split_modes || e->calibrate) {
         const size_t nb_loc = (size_t)e->K_loc / kSumBlock, nb_tot = (size_t)e->K / kSumBlock;
         CREATE_TRY(dev_alloc(e, &e->d_mm, 2 * (size_t)J * N));
         CREATE_TRY(dev_alloc(e, &e->d_psum_part, nb_loc * J * N));
@@ -1473,6 +1609,7 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     }
 #endif
     if (hipStreamSynchronize(e->stream) != hipSuccess) CREATE_TRY(fail(e, STOMP_E_DEVICE, "setup failed"));
+    if (e->calibrate) CREATE_TRY(calibrate_shard_mode(e));
     *out = e;
     return 0;
 #undef CREATE_TRY
@@ -1971,6 +2108,23 @@ int stomp_engine_shard_mode(stomp_engine* e, int32_t* mode)
 {
     if (!e || !mode) return fail(e, STOMP_E_INVALID, "null argument");
     *mode = e->world == 1 ? STOMP_SHARD_NONE : (e->gather ? STOMP_SHARD_GATHER : STOMP_SHARD_PARTIALS);
+    return 0;
+}
+
+int stomp_engine_shard_info(stomp_engine* e, double* info)
+{
+    if (!e || !info) return fail(e, STOMP_E_INVALID, "null argument");
+    for (int k = 0; k < 6; ++k) info[k] = e->shard_info[k];
+    if (!e->calibrate) info[0] = e->world == 1 ? STOMP_SHARD_NONE : (e->gather ? STOMP_SHARD_GATHER : STOMP_SHARD_PARTIALS);
+    return 0;
+}
+
+int stomp_shard_decide(const double* measured, int32_t* mode)
+{
+    if (!measured || !mode) return STOMP_E_INVALID;
+    const double gather = measured[0] + measured[3];
+    const double partials = measured[1] + measured[2] + 2.0 * measured[4];
+    *mode = gather <= partials ? STOMP_SHARD_GATHER : STOMP_SHARD_PARTIALS;
     return 0;
 }
 

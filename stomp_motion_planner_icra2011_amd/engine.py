@@ -91,7 +91,8 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_engine_get_best_torques", "stomp_pi_get_rollouts", "stomp_pi_set_rollout_costs",
             "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_pi_reset", "stomp_sdf_build_objects",
             "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
-            "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy", "stomp_engine_shard_mode"]
+            "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy", "stomp_engine_shard_mode",
+            "stomp_engine_shard_info", "stomp_shard_decide"]
 
 _lib = None
 
@@ -136,6 +137,8 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_get_timing.argtypes = [P, C.c_char_p, dp, C.POINTER(C.c_int32)]
     l.stomp_engine_local_rollouts.argtypes = [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     l.stomp_engine_shard_mode.argtypes = [P, C.POINTER(C.c_int32)]
+    l.stomp_engine_shard_info.argtypes = [P, dp]
+    l.stomp_shard_decide.argtypes = [dp, C.POINTER(C.c_int32)]
     l.stomp_sdf_build.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double, dp, C.c_int32, dp,
                                   C.c_int32, C.c_void_p, C.c_void_p]
     l.stomp_sdf_build_objects.argtypes = [C.c_int32, C.c_int32, C.c_int32, dp, C.c_double, C.c_double,
@@ -314,6 +317,12 @@ class Engine:
         mode = C.c_int32()
         _check(l.stomp_engine_shard_mode(self.h, C.byref(mode)))
         self.shard_mode = {0: "none", 1: "partials", 2: "gather"}[mode.value]
+        info = np.zeros(6)
+        _check(l.stomp_engine_shard_info(self.h, _dp(info)))
+        # measured at creation when both decompositions were possible (stomp_engine_shard_info), us
+        self.shard_info = None if info[1] == 0.0 else dict(
+            t_gather=info[1], t_partials=info[2], l_allreduce=info[3], l_allgather_state=info[4],
+            l_allgather_partials=info[5])
 
     def close(self):
         h = getattr(self, "h", None)
@@ -532,6 +541,14 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(load_library().stomp_comm_unique_id(buf))
     return buf.raw
+
+
+def shard_decide(t_gather, t_partials, l_allreduce, l_allgather_state, l_allgather_partials) -> str:
+    """The engine's decomposition rule on measured times (us), host only (stomp_shard_decide)."""
+    m = np.array([t_gather, t_partials, l_allreduce, l_allgather_state, l_allgather_partials], np.float64)
+    mode = C.c_int32()
+    _check(load_library().stomp_shard_decide(_dp(m), C.byref(mode)))
+    return {1: "partials", 2: "gather"}[mode.value]
 
 
 def comm_local_id(world_size: int) -> bytes:

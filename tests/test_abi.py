@@ -129,3 +129,11 @@ def test_float_field_rejected():
     p.sdf = np.full((16, 16, 16), 70000, np.int64)
     with pytest.raises(ValueError, match="65535"):
         eng.Engine(p)
+
+
+def test_shard_decide_rule():
+    # the K-sharded decomposition from measured times (us): gather posts one all-gather of the
+    # state rows, partials three dependent collectives (stomp_shard_decide)
+    assert eng.shard_decide(51.4, 42.7, 20.0, 25.0, 20.0) == "gather"      # RCCL-like latencies
+    assert eng.shard_decide(51.4, 42.7, 1.0, 2.0, 1.0) == "partials"       # collectives cheaper than the compute gap
+    assert eng.shard_decide(40.0, 40.0, 0.0, 0.0, 0.0) == "gather"         # ties: one collective

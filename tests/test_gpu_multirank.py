@@ -168,6 +168,47 @@ def test_ranks_with_state_terms_bitwise(mode, monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize("world,latency_us", [(2, 0.0), (4, 0.0), (4, 5000.0)])
+def test_decomposition_measured_at_creation(world, latency_us, monkeypatch):
+    # no STOMP_SHARD_MODE: the ranks time both decompositions' compute and their collectives at
+    # creation and take the maxima over the ranks (stomp_engine_shard_info); every rank picks the same
+    # one by stomp_shard_decide's rule.  A synthetic 5 ms per collective makes the one-exchange gather
+    # mode the choice; either way the iterations after the calibration are the oracle's bit for bit
+    monkeypatch.setenv("STOMP_DEBUG_CALIBRATE_LOCAL", "1")
+    monkeypatch.setenv("STOMP_DEBUG_SHARD_LATENCY_US", str(latency_us))
+    monkeypatch.delenv("STOMP_SHARD_MODE", raising=False)
+    p = pb.make_problem(grid_n=64, num_rollouts=256, num_reused_rollouts=0)
+    gid = eng.comm_local_id(world)
+    with cf.ThreadPoolExecutor(world) as ex:   # the calibration exchanges: one host thread per rank
+        engines = list(ex.map(lambda r: eng.Engine(p, rank=r, world_size=world, comm_id=gid), range(world)))
+    modes = {e.shard_mode for e in engines}
+    assert len(modes) == 1, modes
+    info = engines[0].shard_info
+    assert info is not None and all(e.shard_info == info for e in engines)
+    assert engines[0].shard_mode == eng.shard_decide(**info)
+    if latency_us > 0:
+        assert engines[0].shard_mode == "gather"
+    o = po.Oracle(p, threads=THREADS)
+    K_loc = 256 // world
+
+    def drive(r, e):
+        out = []
+        for it in range(1, 4):
+            out.append((e.iterate(it), e.theta(), e.rollouts("state_costs")))
+        return out
+
+    recs = on_threads(engines, drive)
+    for k, it in enumerate(range(1, 4)):
+        oc = o.iterate(it)
+        for r in range(world):
+            c, th, st = recs[r][k]
+            assert c == oc, (it, r)
+            np.testing.assert_array_equal(th, o.theta())
+            np.testing.assert_array_equal(st, o.rollouts("state_costs")[r * K_loc:(r + 1) * K_loc])
+    for e in engines:
+        e.close()
+
+
 def test_gather_request_not_honoured_fails(monkeypatch):
     # STOMP_SHARD_MODE=gather with reused rollouts cannot run gather mode: creation fails instead of
     # silently falling back to partials (a rank on the other mode would post other collectives)
