@@ -161,16 +161,18 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 // joints (BLOCK / 64 waves >= the row's 16-waypoint tiles: one round), M eps on the fp64 matrix
 // cores (mfma_tile: the k-ascending fma chains of the rollout kernel's noise phase, band_product's
 // sums bit for bit), x = params + M eps, then rollout_control (control_term / control_cost's
-// expressions).  REUSE: the row is not copied yet; the workgroup of reused row rr ranks the
-// candidates from their totals (k_reuse's (cost, index) order, the extra rollout at -1), takes
-// the candidate of rank rr and writes its params, the noise params - theta and its state row
-// (k_reuse's copy), then prices it from registers and LDS.  The K previous rows' totals come from
-// the rollout launch's totals blocks; the extra rollout's is made here (candidate_total).
+// expressions).  REUSE: the row is not copied yet; the workgroup of reused row rr finds the
+// candidate of rank rr in k_reuse's (cost, index) order (the extra rollout at -1), writes its
+// params, the noise params - theta and its state row (k_reuse's copy), then prices it from
+// registers and LDS.  The K previous rows' totals come from the rollout launch's totals blocks;
+// the extra rollout's is made here (candidate_total's stage and sums), overlapped with the loads
+// of the two rows rank rr can be besides the extra rollout's (see the prologue).
+constexpr int kReuseRowsMax = 1024;   // candidates the reused rows' kernel ranks itself
+
 template <int BLOCK, int NG, bool REUSE>
 __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
 {
     extern __shared__ __attribute__((aligned(16))) double lds_nr[];
-    __shared__ int src_sel;
     if (a.stop && *a.stop) return;
     const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J), NB = N + kBandBatch;
     const int r = a.row_begin + blockIdx.x;
@@ -183,57 +185,173 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
     STAMP(0);
     const double* psrc = a.params + row;
     const double* nsrc = a.noise + row;
-    if constexpr (REUSE) {
-        const int n = ra.K + ra.with_extra, rr = r - ra.K_gen;
-        double* costs = prm + J * N;   // [n]: the K previous rows' totals (the rollout launch's), the extra's
-        for (int i = tid; i < ra.K; i += BLOCK) costs[i] = ra.costs[i];
-        if (ra.with_extra) {
-            // the extra (noiseless) rollout's total, evaluated by this iteration's rollout launch;
-            // xs and cs are its stage (dead until the projection)
-            const double t = candidate_total<BLOCK>(ra.x_state, ra.x_control, J, N, xs, tid);
-            if (tid == 0) costs[ra.K] = t;
-        }
-        __syncthreads();
-        for (int c = tid; c < n; c += BLOCK) {
-            const int ic = c < ra.K ? c : -1;
-            const double cc = costs[c];
-            int rank = 0;
-            for (int c0 = 0; c0 < n; c0 += 8) {
-                double x[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = costs[min(c0 + u, n - 1)];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int c2 = c0 + u, ic2 = c2 < ra.K ? c2 : -1;
-                    if (c2 < n && (x[u] < cc || (x[u] == cc && ic2 < ic))) ++rank;
-                }
-            }
-            if (rank == rr) src_sel = c;   // ranks are a permutation: one writer
-        }
-        __syncthreads();
-        const int src = src_sel;
-        psrc = src < ra.K ? ra.src_params + (size_t)src * J * N : ra.x_params;
-        const double* ssrc = src < ra.K ? ra.src_state + (size_t)src * N : ra.x_state;
-        for (int i = tid; i < N; i += BLOCK) ra.state[(size_t)r * N + i] = ssrc[i];
-    }
     // the noise and params rows: every load of the workgroup in flight at once (coalesced)
     constexpr int kRowLoads = 4096 / BLOCK;   // the row in few passes
-    for (int i0 = tid; i0 - tid < J * N; i0 += kRowLoads * BLOCK) {
+    const int JN = J * N;
+    int first = tid;                          // the generic passes start here
+    if constexpr (REUSE) {
+        // Two dependent memory round trips instead of four: (1) everything that depends on nothing
+        // (the K totals, the extra rollout's cost rows, theta, the extra rollout's params and
+        // state rows); (2) each wave ranks the K previous rows by their totals alone and loads
+        // the rows of K-rank rr and rr - 1, then wave 0 runs the extra rollout's t-chains.
+        // Inserting the extra rollout (index -1: ahead of equal totals) into the K-order moves
+        // rank rr to K-rank rr (its total < the extra's), to the extra, or to K-rank rr - 1 (its
+        // total >= the extra's): k_reuse's (cost, index) order, decided from two compares.
+        constexpr int kCostLoads = (kReuseRowsMax + BLOCK - 1) / BLOCK;
+        const int K = ra.K, rr = r - ra.K_gen, L = J + 1, P = L * N;
+        const bool wx = ra.with_extra;
+        double* costs = prm + JN;   // [K + 7] the previous rows' totals (the rollout launch's), inf
+        double* stage = xs;         // [J + 1][N] the extra rollout's cost rows (xs, cs: dead until the projection)
+        __shared__ double part[kMaxJoints + 1];
+        __shared__ int sel[2];
+        double cv[kCostLoads], th[kRowLoads], px[kRowLoads], pa[kRowLoads], pb[kRowLoads];
+        double sx = 0.0, sa, sb;
+        const int ti = min(tid, N - 1);
+        // a wave issues only the loads of its own live elements (wave-uniform skips: the row's
+        // JN elements are ~1.4 per lane at cfg1, and each clamped duplicate load still costs
+        // the CU's address and data path)
+        const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+        auto live = [&](int u, int n) { return wbase + u * BLOCK < n; };
+#pragma unroll
+        for (int u = 0; u < kCostLoads; ++u)
+            if (live(u, K)) cv[u] = ra.costs[min(tid + u * BLOCK, K - 1)];
+#pragma unroll
+        for (int u = 0; u < kRowLoads; ++u)
+            if (live(u, JN)) th[u] = a.theta[min(tid + u * BLOCK, JN - 1)];
+        if (wx) {
+#pragma unroll
+            for (int u = 0; u < kRowLoads; ++u)
+                if (live(u, JN)) px[u] = ra.x_params[min(tid + u * BLOCK, JN - 1)];
+            sx = ra.x_state[ti];
+            for (int i0 = tid; i0 - tid < P; i0 += 4 * BLOCK) {   // candidate_total's stage
+                double v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int idx = min(i0 + u * BLOCK, P - 1);
+                    if (live(u, P - (i0 - tid))) v[u] = idx < N ? ra.x_state[idx] : ra.x_control[idx - N];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i0 + u * BLOCK < P) stage[i0 + u * BLOCK] = v[u];
+            }
+        }
+        // the totals, then +inf up to a multiple of 8 (ranks past K count nothing: inf is below
+        // no total, and equals only an inf total of a lower index)
+#pragma unroll
+        for (int u = 0; u < kCostLoads; ++u) {
+            const int c = tid + u * BLOCK;
+            if (c < K) costs[c] = cv[u];
+            else if (c < ((K + 7) & ~7)) costs[c] = __builtin_inf();
+        }
+        __syncthreads();
+        STAMP(6);
+        // K-rank of candidate c: (total, index) ascending among the K previous rows
+        auto k_rank = [&](int c) {
+            const double cc = costs[c];
+            int rank = 0;
+            for (int c0 = 0; c0 < K; c0 += 8) {
+                double x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = costs[c0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)   // branch-free
+                    rank += (int)((x[u] < cc) | ((x[u] == cc) & (c0 + u < c)));
+            }
+            return rank;
+        };
+        int selA, selB;
+        if (K <= 64) {   // every wave ranks all K itself: no barrier before the row loads
+            const int lane = tid & 63;
+            const int rank = lane < K ? k_rank(lane) : -2;
+            const unsigned long long ma = __ballot(rank == rr), mb = __ballot(rank == rr - 1);
+            selA = __builtin_amdgcn_readfirstlane(__ffsll((long long)ma) - 1);
+            selB = rr > 0 ? __builtin_amdgcn_readfirstlane(__ffsll((long long)mb) - 1) : selA;
+        } else {
+            for (int c = tid; c < K; c += BLOCK) {
+                const int rank = k_rank(c);
+                if (rank == rr) sel[0] = c;       // ranks are a permutation: one writer each
+                if (rank == rr - 1) sel[1] = c;
+            }
+            __syncthreads();
+            selA = sel[0];
+            selB = rr > 0 ? sel[1] : selA;
+        }
+        STAMP(10);
+        const double* rA = ra.src_params + (size_t)selA * JN;
+        const double* rB = ra.src_params + (size_t)selB * JN;
+#pragma unroll
+        for (int u = 0; u < kRowLoads; ++u) {
+            const int idx = min(tid + u * BLOCK, JN - 1);
+            if (live(u, JN)) {
+                pa[u] = rA[idx];
+                pb[u] = rB[idx];
+            }
+        }
+        sa = ra.src_state[(size_t)selA * N + ti];
+        sb = ra.src_state[(size_t)selB * N + ti];
+        STAMP(11);
+        if (wx && tid < L) {
+            // Rollout::getCost's t-chain of the extra rollout's row (tid & 63): x = v[0], then
+            // x += v[t] ascending (candidate_total's order)
+            const double* v = stage + (size_t)tid * N;
+            double x = v[0];
+            int t = 1;
+            for (; t + 16 <= N; t += 16) {
+                double b[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) b[u] = v[t + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) x += b[u];
+            }
+            for (; t < N; ++t) x += v[t];
+            part[tid] = x;
+        }
+        STAMP(12);
+        __syncthreads();
+        STAMP(7);
+        int src = selA;   // K: the extra rollout
+        if (wx) {
+            double xt = part[0];
+            for (int d = 0; d < J; ++d) xt += part[1 + d];
+            if (xt != xt) xt = __builtin_inf();
+            if (!(costs[selA] < xt)) src = (rr > 0 && costs[selB] >= xt) ? selB : K;
+        }
+        const int pick = src == selA ? 0 : (src == selB ? 1 : 2);
+        if (tid < N) ra.state[(size_t)r * N + tid] = pick == 0 ? sa : (pick == 1 ? sb : sx);
+#pragma unroll
+        for (int u = 0; u < kRowLoads; ++u) {
+            const int idx = tid + u * BLOCK;
+            if (idx < JN) {
+                const int d = idx / N, k = idx - d * N;
+                const double p = pick == 0 ? pa[u] : (pick == 1 ? pb[u] : px[u]);
+                const double e = p - th[u];   // k_reuse's copy: params, noise = params - theta
+                a.params[row + idx] = p;
+                a.noise[row + idx] = e;
+                eps[k * JP + d] = e;
+                prm[idx] = p;
+            }
+        }
+        psrc = src < K ? ra.src_params + (size_t)src * JN : ra.x_params;
+        const double* ssrc = src < K ? ra.src_state + (size_t)src * N : ra.x_state;
+        for (int i = tid + BLOCK; i < N; i += BLOCK) ra.state[(size_t)r * N + i] = ssrc[i];
+        first = tid + kRowLoads * BLOCK;
+    }
+    for (int i0 = first; i0 - tid < JN; i0 += kRowLoads * BLOCK) {
         double ve[kRowLoads], vp[kRowLoads];
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
-            const int idx = min(i0 + u * BLOCK, J * N - 1);
+            const int idx = min(i0 + u * BLOCK, JN - 1);
             vp[u] = psrc[idx];
             ve[u] = REUSE ? a.theta[idx] : nsrc[idx];
         }
 #pragma unroll
         for (int u = 0; u < kRowLoads; ++u) {
             const int idx = i0 + u * BLOCK;
-            if (idx < J * N) {
+            if (idx < JN) {
                 const int d = idx / N, k = idx - d * N;
                 double e = ve[u];
                 if constexpr (REUSE) {
-                    e = vp[u] - ve[u];   // k_reuse's copy: params, noise = params - theta
+                    e = vp[u] - ve[u];
                     a.params[row + idx] = vp[u];
                     a.noise[row + idx] = e;
                 }
@@ -269,7 +387,6 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
 }
 
 namespace {
-constexpr int kReuseRowsMax = 1024;   // candidates the reused rows' kernel ranks itself
 
 size_t noise_rows_lds(const NoiseArgs& a, int n)
 {
@@ -301,14 +418,14 @@ void launch_noise_rows(const NoiseArgs& a, const ReuseArgs& ra, int rows, size_t
 bool launch_reuse_rows_ok(const NoiseArgs& a, int K, int Kr)
 {
     return !a.zero_noise && a.first_global == 0 && a.row_begin >= a.K_gen_global && a.K_loc - a.row_begin == Kr &&
-           a.J <= 4 * kNoiseJT && K + 1 <= kReuseRowsMax && noise_rows_lds(a, K + 1) <= kRolloutLdsMax;
+           a.J <= 4 * kNoiseJT && K + 1 <= kReuseRowsMax && noise_rows_lds(a, K + 8) <= kRolloutLdsMax;
 }
 
 void launch_reuse_rows(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s)
 {
     const int rows = a.K_loc - a.row_begin;
     if (rows <= 0) return;
-    launch_noise_rows<true>(a, ra, rows, noise_rows_lds(a, ra.K + ra.with_extra), s);
+    launch_noise_rows<true>(a, ra, rows, noise_rows_lds(a, ra.K + 8), s);   // the totals + inf padding
 }
 
 STOMP_STAMP_ACCESSORS(noise)

@@ -73,7 +73,7 @@ def cost_label(i):
 show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch (odd: FK on waves 2-3)
 show("cost", 2, cost_label)   # an even one (FK on waves 0-1, thread 0 stamps inside the FK lanes)
 show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
-NOISE_LABELS = {0: "start", 1: "rows loaded / normals", 2: "M eps (rows) / L z", 3: "M eps", 4: "control", 5: "end",
+NOISE_LABELS = {0: "start", 6: "reuse: loads in, staged", 10: "reuse: K-ranked", 11: "reuse: row loads issued", 12: "reuse: t-chains (wave 0)", 7: "reuse: barrier", 1: "rows loaded / normals", 2: "M eps (rows) / L z", 3: "M eps", 4: "control", 5: "end",
                 9: "control: padding", 61: "control terms (thread 0)", 62: "control terms barrier",
                 63: "control costs stored (t0)"}
 show("noise", 0, lambda i: NOISE_LABELS.get(i, str(i)))
