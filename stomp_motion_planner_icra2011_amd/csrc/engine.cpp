@@ -146,6 +146,10 @@ struct stomp_engine {
     double *d_tot_loc = nullptr, *d_tot_all = nullptr, *d_tot_x = nullptr, *d_slot = nullptr, *d_slot_all = nullptr;
     double* d_reuse_costs = nullptr;   // one device: k_reuse's totals [K + 1] and its counter
     int* d_reuse_count = nullptr;
+    // one device, reuse: every candidate priced ahead by the rollout launch (CostArgs::spec_*),
+    // [K + 1][J][N] each (row K the extra rollout); spec_on: allocated (STOMP_DEBUG_NO_SPEC=1: not)
+    double *d_spec_params = nullptr, *d_spec_noise = nullptr, *d_spec_ctl = nullptr;
+    bool spec_on = false;
     int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
     uint16_t* d_sdf = nullptr;   // d2 per voxel
@@ -736,6 +740,14 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         Timed tm(e, T_NOISE);
         launch_noise(na, e->stream);
     }
+    // the candidates priced by the rollout launch (launch_reuse_pick) when its blocks still fit
+    // the CUs beside the rollouts, pregen and totals blocks (more pricing blocks than idle CUs
+    // would lengthen the launch)
+    const int spec_nro = num_gen + (e->pending_member >= 0 ? 1 : 0);
+    const int spec_extra = (pre ? e->rows : 0) + e->K + (e->K + 1);
+    const bool spec = reuse_late && e->spec_on && e->world == 1 && launch_reuse_pick_ok(na, e->K, e->Kr) &&
+                      spec_nro + spec_extra <= e->model.cus &&
+                      rollout_split_pieces(e->model, spec_nro, spec_extra, true) > 0;
     // Task::execute for the generated rollouts of this shard (+ the pending noiseless rollout)
     {
         CostArgs ca{};
@@ -757,6 +769,13 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             // the reuse candidates' totals (the previous rows, complete) made beside the rollouts
             ca.tot_rows = e->K;
             ca.tot_state = e->d_state_b; ca.tot_control = e->d_control_b; ca.tot_out = e->d_reuse_costs;
+            if (spec) {
+                // and every candidate re-based on theta and priced, so that the reuse step only
+                // ranks and copies
+                ca.spec_rows = e->K + 1;
+                ca.spec_src = e->d_params_b;
+                ca.spec_params = e->d_spec_params; ca.spec_noise = e->d_spec_noise; ca.spec_ctl = e->d_spec_ctl;
+            }
         }
         if (e->terms_on) ca.traj_out = e->d_terms_traj;
         if (e->pending_member >= 0) {
@@ -797,7 +816,12 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             ra.x_params = e->d_x_params; ra.x_state = e->d_x_state; ra.x_control = e->d_x_control;
             ra.state = e->d_state;
             Timed tm(e, T_NOISE);
-            launch_reuse_rows(na, ra, e->stream);
+            if (spec) {
+                ra.spec_params = e->d_spec_params; ra.spec_noise = e->d_spec_noise; ra.spec_ctl = e->d_spec_ctl;
+                launch_reuse_pick(na, ra, e->stream);
+            } else {
+                launch_reuse_rows(na, ra, e->stream);
+            }
         } else {
             if (int rc = run_reuse(e)) return rc;
             if (na.row_begin < na.K_loc) {
@@ -1280,6 +1304,14 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     if (e->world == 1 && e->Kr > 0) {   // k_reuse's per-candidate totals and its counter (zeroed)
         CREATE_TRY(dev_alloc(e, &e->d_reuse_costs, (size_t)e->K + 1));
         CREATE_TRY(dev_alloc(e, &e->d_reuse_count, 1));
+        const char* no_spec = std::getenv("STOMP_DEBUG_NO_SPEC");
+        if (!(no_spec && std::strcmp(no_spec, "1") == 0)) {
+            const size_t n = ((size_t)e->K + 1) * J * N;
+            CREATE_TRY(dev_alloc(e, &e->d_spec_params, n));
+            CREATE_TRY(dev_alloc(e, &e->d_spec_noise, n));
+            CREATE_TRY(dev_alloc(e, &e->d_spec_ctl, n));
+            e->spec_on = true;
+        }
     }
     if (e->world > 1 && e->Kr > 0) {
         const size_t slot = (size_t)e->Kr * ((size_t)J * N + N);

@@ -221,6 +221,25 @@ __device__ __forceinline__ void totals_block(const CostArgs& a, int J, int N, in
     if (threadIdx.x == 0) a.tot_out[c] = t;
 }
 
+// a split rollout launch's block past its totals blocks: reuse candidate c priced ahead of the
+// ranking (price_candidate into the spec rows; c = spec_rows - 1 is the extra rollout, params
+// theta); lds: the workgroup's whole dynamic LDS (at least price_candidate_lds_bytes).  Only the
+// split kernel carries these blocks (rollout_split_pieces): inlined into the slot-loop kernels the
+// pricing code pushed them into scratch.
+template <int BLOCK>
+__device__ __forceinline__ void spec_block(const CostArgs& a, int c, double* lds)
+{
+    if (a.stop && *a.stop) return;
+    const size_t JN = (size_t)a.nz.J * a.nz.N;
+    const double* psrc = c < a.spec_rows - 1 ? a.spec_src + c * JN : nullptr;
+    if (a.nz.J <= 2 * kNoiseJT)
+        price_candidate<BLOCK, 2>(a.nz, psrc, a.spec_params + c * JN, a.spec_noise + c * JN, a.spec_ctl + c * JN, lds,
+                                  threadIdx.x);
+    else
+        price_candidate<BLOCK, 4>(a.nz, psrc, a.spec_params + c * JN, a.spec_noise + c * JN, a.spec_ctl + c * JN, lds,
+                                  threadIdx.x);
+}
+
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
 // FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
@@ -866,7 +885,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
     double* zB = (double*)(lds_raw + L.zB);
     if (bid >= nro * P) {
         const int r = bid - nro * P;
-        if (r >= a.pre_rows) totals_block<BLOCK>(a, J, N, r - a.pre_rows, zA);   // zA, zB: contiguous
+        if (r >= a.pre_rows + a.tot_rows) spec_block<BLOCK>(a, r - a.pre_rows - a.tot_rows, (double*)lds_raw);
+        else if (r >= a.pre_rows) totals_block<BLOCK>(a, J, N, r - a.pre_rows, zA);   // zA, zB: contiguous
         else pregen_block<BLOCK>(a, r, false, zA, zB);
         return;
     }
@@ -1210,6 +1230,20 @@ size_t rollout_split_lds_bytes(const DevModel& m, int P)
     return split_lds(m.J, m.N, m.S, m.nsaves, m.nslots, W, Wo, R.pad - R.sph).total;
 }
 
+// the split launch's dynamic LDS: the split body's, or a pricing block's if larger
+size_t rollout_split_launch_lds(const DevModel& m, int P, bool spec)
+{
+    const size_t ls = rollout_split_lds_bytes(m, P);
+    return spec ? std::max(ls, price_candidate_lds_bytes(m.J, m.N)) : ls;
+}
+
+int rollout_split_pieces(const DevModel& m, int nro, int extra_blocks, bool spec)
+{
+    const int P = split_pieces(m, nro, extra_blocks);
+    if (!P || rollout_split_launch_lds(m, P, spec) + 1024 > kRolloutLdsMax) return 0;
+    return P;
+}
+
 STOMP_STAMP_ACCESSORS(cost)
 
 // generateRollouts' normals and eps = sigma L z, computeProjectedNoise's M eps for one row per
@@ -1317,22 +1351,22 @@ template <bool BRICK>
 static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
     const int nro = a.num_noisy + (a.x_params ? 1 : 0);
-    const int extra_blocks = (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows;   // pregen, then totals
+    // pregen, then totals, then the priced candidates (split launches only)
+    const int extra_blocks = (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows + a.spec_rows;
     const int blocks = nro + extra_blocks;
     const size_t lds = rollout_lds_bytes(m, m.pad_lds);
-    if (const int P = split_pieces(m, nro, extra_blocks)) {
-        const size_t ls = rollout_split_lds_bytes(m, P);
-        if (ls + 1024 <= kRolloutLdsMax) {
-            assert(nro <= m.split_cap);   // split_pieces keeps nro within the counters
-            CostArgs b = a;
-            b.split = P;
-            b.split_cnt = m.split_cnt;
-            lds_opt_in((const void*)k_rollout_split<kSplitBlock, BRICK>, ls);
-            hipLaunchKernelGGL((k_rollout_split<kSplitBlock, BRICK>), dim3(nro * P + extra_blocks), dim3(kSplitBlock),
-                               ls, s, m, b);
-            return;
-        }
+    if (const int P = rollout_split_pieces(m, nro, extra_blocks, a.spec_rows > 0)) {
+        const size_t ls = rollout_split_launch_lds(m, P, a.spec_rows > 0);
+        assert(nro <= m.split_cap);   // split_pieces keeps nro within the counters
+        CostArgs b = a;
+        b.split = P;
+        b.split_cnt = m.split_cnt;
+        lds_opt_in((const void*)k_rollout_split<kSplitBlock, BRICK>, ls);
+        hipLaunchKernelGGL((k_rollout_split<kSplitBlock, BRICK>), dim3(nro * P + extra_blocks), dim3(kSplitBlock), ls,
+                           s, m, b);
+        return;
     }
+    assert(a.spec_rows == 0);   // the engine asks rollout_split_pieces first
     if (kWideBlock != kBlock && nro <= m.cus && m.phased_lds > 0) {
         const size_t lp = m.phased_lds;
         lds_opt_in((const void*)k_rollout_phased<BRICK>, lp);
@@ -1350,7 +1384,8 @@ static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
 
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s)
 {
-    if (a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows <= 0) return;
+    if (a.num_noisy + (a.x_params ? 1 : 0) + (a.pre_rows > 0 ? a.pre_rows : 0) + a.tot_rows + a.spec_rows <= 0)
+        return;
     if (m.brick) launch_cost_t<true>(m, a, s);
     else launch_cost_t<false>(m, a, s);
 }

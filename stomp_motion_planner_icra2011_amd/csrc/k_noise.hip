@@ -156,6 +156,121 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
     STAMP(5);
 }
 
+// k_reuse's choice for reused row rr (policy_improvement.cpp:176-225) in two dependent memory
+// round trips: (1) the K totals and the extra rollout's J + 1 cost rows (its total's stage), with
+// the caller's independent loads (`independent`) in flight beside them; (2) each wave ranks the K
+// previous rows by their totals alone (one wave per 64: no barrier before the caller's loads of
+// the rows of K-rank rr and rr - 1, `dependent(A, B)`), while wave 0 runs the extra rollout's
+// t-chains.  Inserting the extra rollout (index -1: ahead of equal totals) into the K-order moves
+// rank rr to K-rank rr (its total < the extra's), to the extra, or to K-rank rr - 1 (its total >=
+// the extra's): k_reuse's (cost, index) order, decided from two compares.  Returns the candidate
+// (K: the extra rollout).  LDS: costs [K rounded up to 8], stage [(J + 1) N].
+constexpr int kReuseRowsMax = 1024;   // candidates the reused rows' kernels rank themselves
+
+template <int BLOCK, class Independent, class Dependent>
+__device__ __forceinline__ int reuse_choice(const ReuseArgs& ra, int J, int N, int rr, double* costs, double* stage,
+                                            int tid, Independent&& independent, Dependent&& dependent)
+{
+    constexpr int kCostLoads = (kReuseRowsMax + BLOCK - 1) / BLOCK;
+    const int K = ra.K, L = J + 1, P = L * N;
+    const bool wx = ra.with_extra;
+    __shared__ double part[kMaxJoints + 1];
+    __shared__ int sel[2];
+    double cv[kCostLoads];
+    // a wave issues only the loads of its own live elements (wave-uniform skips: a row's JN
+    // elements are ~1.4 per lane at cfg1, and each clamped duplicate load still costs the CU's
+    // address and data path)
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+#pragma unroll
+    for (int u = 0; u < kCostLoads; ++u)
+        if (wbase + u * BLOCK < K) cv[u] = ra.costs[min(tid + u * BLOCK, K - 1)];
+    independent();
+    if (wx) {
+        for (int i0 = tid; i0 - tid < P; i0 += 4 * BLOCK) {   // candidate_total's stage
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int idx = min(i0 + u * BLOCK, P - 1);
+                if (wbase + u * BLOCK < P - (i0 - tid)) v[u] = idx < N ? ra.x_state[idx] : ra.x_control[idx - N];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * BLOCK < P) stage[i0 + u * BLOCK] = v[u];
+        }
+    }
+    // the totals, then +inf up to a multiple of 8 (ranks past K count nothing: inf is below no
+    // total, and equals only an inf total of a lower index)
+#pragma unroll
+    for (int u = 0; u < kCostLoads; ++u) {
+        const int c = tid + u * BLOCK;
+        if (c < K) costs[c] = cv[u];
+        else if (c < ((K + 7) & ~7)) costs[c] = __builtin_inf();
+    }
+    __syncthreads();
+    STAMP(6);
+    // K-rank of candidate c: (total, index) ascending among the K previous rows
+    auto k_rank = [&](int c) {
+        const double cc = costs[c];
+        int rank = 0;
+        for (int c0 = 0; c0 < K; c0 += 8) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = costs[c0 + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)   // branch-free
+                rank += (int)((x[u] < cc) | ((x[u] == cc) & (c0 + u < c)));
+        }
+        return rank;
+    };
+    int selA, selB;
+    if (K <= 64) {   // every wave ranks all K itself: no barrier before the row loads
+        const int lane = tid & 63;
+        const int rank = lane < K ? k_rank(lane) : -2;
+        const unsigned long long ma = __ballot(rank == rr), mb = __ballot(rank == rr - 1);
+        selA = __builtin_amdgcn_readfirstlane(__ffsll((long long)ma) - 1);
+        selB = rr > 0 ? __builtin_amdgcn_readfirstlane(__ffsll((long long)mb) - 1) : selA;
+    } else {
+        for (int c = tid; c < K; c += BLOCK) {
+            const int rank = k_rank(c);
+            if (rank == rr) sel[0] = c;       // ranks are a permutation: one writer each
+            if (rank == rr - 1) sel[1] = c;
+        }
+        __syncthreads();
+        selA = sel[0];
+        selB = rr > 0 ? sel[1] : selA;
+    }
+    STAMP(10);
+    dependent(selA, selB);
+    STAMP(11);
+    if (wx && tid < L) {
+        // Rollout::getCost's t-chain of the extra rollout's row tid: x = v[0], then x += v[t]
+        // ascending (candidate_total's order)
+        const double* v = stage + (size_t)tid * N;
+        double x = v[0];
+        int t = 1;
+        for (; t + 16 <= N; t += 16) {
+            double b[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) b[u] = v[t + u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) x += b[u];
+        }
+        for (; t < N; ++t) x += v[t];
+        part[tid] = x;
+    }
+    STAMP(12);
+    __syncthreads();
+    STAMP(7);
+    int src = selA;
+    if (wx) {
+        double xt = part[0];
+        for (int d = 0; d < J; ++d) xt += part[1 + d];
+        if (xt != xt) xt = __builtin_inf();
+        if (!(costs[selA] < xt)) src = (rr > 0 && costs[selB] >= xt) ? selB : K;
+    }
+    return src;
+}
+
 // The reused rows of an iteration (policy_improvement.cpp:208-224: noise re-based on theta),
 // then computeProjectedNoise (:473-482) and computeControlCosts: one workgroup per row and all its
 // joints (BLOCK / 64 waves >= the row's 16-waypoint tiles: one round), M eps on the fp64 matrix
@@ -167,8 +282,6 @@ __global__ __launch_bounds__(BLOCK) void k_noise(NoiseArgs a)
 // registers and LDS.  The K previous rows' totals come from the rollout launch's totals blocks;
 // the extra rollout's is made here (candidate_total's stage and sums), overlapped with the loads
 // of the two rows rank rr can be besides the extra rollout's (see the prologue).
-constexpr int kReuseRowsMax = 1024;   // candidates the reused rows' kernel ranks itself
-
 template <int BLOCK, int NG, bool REUSE>
 __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
 {
@@ -190,132 +303,46 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
     const int JN = J * N;
     int first = tid;                          // the generic passes start here
     if constexpr (REUSE) {
-        // Two dependent memory round trips instead of four: (1) everything that depends on nothing
-        // (the K totals, the extra rollout's cost rows, theta, the extra rollout's params and
-        // state rows); (2) each wave ranks the K previous rows by their totals alone and loads
-        // the rows of K-rank rr and rr - 1, then wave 0 runs the extra rollout's t-chains.
-        // Inserting the extra rollout (index -1: ahead of equal totals) into the K-order moves
-        // rank rr to K-rank rr (its total < the extra's), to the extra, or to K-rank rr - 1 (its
-        // total >= the extra's): k_reuse's (cost, index) order, decided from two compares.
-        constexpr int kCostLoads = (kReuseRowsMax + BLOCK - 1) / BLOCK;
-        const int K = ra.K, rr = r - ra.K_gen, L = J + 1, P = L * N;
+        // the choice with theta and the extra rollout's rows loaded beside the totals, the two
+        // K-ranked candidates' rows beside the t-chains (reuse_choice)
+        const int K = ra.K, rr = r - ra.K_gen;
         const bool wx = ra.with_extra;
         double* costs = prm + JN;   // [K + 7] the previous rows' totals (the rollout launch's), inf
-        double* stage = xs;         // [J + 1][N] the extra rollout's cost rows (xs, cs: dead until the projection)
-        __shared__ double part[kMaxJoints + 1];
-        __shared__ int sel[2];
-        double cv[kCostLoads], th[kRowLoads], px[kRowLoads], pa[kRowLoads], pb[kRowLoads];
+        double th[kRowLoads], px[kRowLoads], pa[kRowLoads], pb[kRowLoads];
         double sx = 0.0, sa, sb;
         const int ti = min(tid, N - 1);
-        // a wave issues only the loads of its own live elements (wave-uniform skips: the row's
-        // JN elements are ~1.4 per lane at cfg1, and each clamped duplicate load still costs
-        // the CU's address and data path)
         const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
-        auto live = [&](int u, int n) { return wbase + u * BLOCK < n; };
-#pragma unroll
-        for (int u = 0; u < kCostLoads; ++u)
-            if (live(u, K)) cv[u] = ra.costs[min(tid + u * BLOCK, K - 1)];
-#pragma unroll
-        for (int u = 0; u < kRowLoads; ++u)
-            if (live(u, JN)) th[u] = a.theta[min(tid + u * BLOCK, JN - 1)];
-        if (wx) {
-#pragma unroll
-            for (int u = 0; u < kRowLoads; ++u)
-                if (live(u, JN)) px[u] = ra.x_params[min(tid + u * BLOCK, JN - 1)];
-            sx = ra.x_state[ti];
-            for (int i0 = tid; i0 - tid < P; i0 += 4 * BLOCK) {   // candidate_total's stage
-                double v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int idx = min(i0 + u * BLOCK, P - 1);
-                    if (live(u, P - (i0 - tid))) v[u] = idx < N ? ra.x_state[idx] : ra.x_control[idx - N];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (i0 + u * BLOCK < P) stage[i0 + u * BLOCK] = v[u];
-            }
-        }
-        // the totals, then +inf up to a multiple of 8 (ranks past K count nothing: inf is below
-        // no total, and equals only an inf total of a lower index)
-#pragma unroll
-        for (int u = 0; u < kCostLoads; ++u) {
-            const int c = tid + u * BLOCK;
-            if (c < K) costs[c] = cv[u];
-            else if (c < ((K + 7) & ~7)) costs[c] = __builtin_inf();
-        }
-        __syncthreads();
-        STAMP(6);
-        // K-rank of candidate c: (total, index) ascending among the K previous rows
-        auto k_rank = [&](int c) {
-            const double cc = costs[c];
-            int rank = 0;
-            for (int c0 = 0; c0 < K; c0 += 8) {
-                double x[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = costs[c0 + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)   // branch-free
-                    rank += (int)((x[u] < cc) | ((x[u] == cc) & (c0 + u < c)));
-            }
-            return rank;
-        };
+        auto live = [&](int u) { return wbase + u * BLOCK < JN; };
         int selA, selB;
-        if (K <= 64) {   // every wave ranks all K itself: no barrier before the row loads
-            const int lane = tid & 63;
-            const int rank = lane < K ? k_rank(lane) : -2;
-            const unsigned long long ma = __ballot(rank == rr), mb = __ballot(rank == rr - 1);
-            selA = __builtin_amdgcn_readfirstlane(__ffsll((long long)ma) - 1);
-            selB = rr > 0 ? __builtin_amdgcn_readfirstlane(__ffsll((long long)mb) - 1) : selA;
-        } else {
-            for (int c = tid; c < K; c += BLOCK) {
-                const int rank = k_rank(c);
-                if (rank == rr) sel[0] = c;       // ranks are a permutation: one writer each
-                if (rank == rr - 1) sel[1] = c;
-            }
-            __syncthreads();
-            selA = sel[0];
-            selB = rr > 0 ? sel[1] : selA;
-        }
-        STAMP(10);
-        const double* rA = ra.src_params + (size_t)selA * JN;
-        const double* rB = ra.src_params + (size_t)selB * JN;
+        const int src = reuse_choice<BLOCK>(
+            ra, J, N, rr, costs, xs, tid,   // stage: xs, cs (dead until the projection)
+            [&]() {
 #pragma unroll
-        for (int u = 0; u < kRowLoads; ++u) {
-            const int idx = min(tid + u * BLOCK, JN - 1);
-            if (live(u, JN)) {
-                pa[u] = rA[idx];
-                pb[u] = rB[idx];
-            }
-        }
-        sa = ra.src_state[(size_t)selA * N + ti];
-        sb = ra.src_state[(size_t)selB * N + ti];
-        STAMP(11);
-        if (wx && tid < L) {
-            // Rollout::getCost's t-chain of the extra rollout's row (tid & 63): x = v[0], then
-            // x += v[t] ascending (candidate_total's order)
-            const double* v = stage + (size_t)tid * N;
-            double x = v[0];
-            int t = 1;
-            for (; t + 16 <= N; t += 16) {
-                double b[16];
+                for (int u = 0; u < kRowLoads; ++u)
+                    if (live(u)) th[u] = a.theta[min(tid + u * BLOCK, JN - 1)];
+                if (wx) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) b[u] = v[t + u];
+                    for (int u = 0; u < kRowLoads; ++u)
+                        if (live(u)) px[u] = ra.x_params[min(tid + u * BLOCK, JN - 1)];
+                    sx = ra.x_state[ti];
+                }
+            },
+            [&](int A, int B) {
+                selA = A;
+                selB = B;
+                const double* rA = ra.src_params + (size_t)A * JN;
+                const double* rB = ra.src_params + (size_t)B * JN;
 #pragma unroll
-                for (int u = 0; u < 16; ++u) x += b[u];
-            }
-            for (; t < N; ++t) x += v[t];
-            part[tid] = x;
-        }
-        STAMP(12);
-        __syncthreads();
-        STAMP(7);
-        int src = selA;   // K: the extra rollout
-        if (wx) {
-            double xt = part[0];
-            for (int d = 0; d < J; ++d) xt += part[1 + d];
-            if (xt != xt) xt = __builtin_inf();
-            if (!(costs[selA] < xt)) src = (rr > 0 && costs[selB] >= xt) ? selB : K;
-        }
+                for (int u = 0; u < kRowLoads; ++u) {
+                    const int idx = min(tid + u * BLOCK, JN - 1);
+                    if (live(u)) {
+                        pa[u] = rA[idx];
+                        pb[u] = rB[idx];
+                    }
+                }
+                sa = ra.src_state[(size_t)A * N + ti];
+                sb = ra.src_state[(size_t)B * N + ti];
+            });
         const int pick = src == selA ? 0 : (src == selB ? 1 : 2);
         if (tid < N) ra.state[(size_t)r * N + tid] = pick == 0 ? sa : (pick == 1 ? sb : sx);
 #pragma unroll
@@ -386,6 +413,91 @@ __global__ __launch_bounds__(BLOCK) void k_noise_rows(NoiseArgs a, ReuseArgs ra)
     STAMP(5);
 }
 
+
+// The reuse step when the rollout launch priced every candidate ahead (CostArgs::spec_*,
+// price_candidate: candidate c's row re-based on theta, M eps and control costs; row K the extra
+// rollout): the workgroup of reused row rr makes the choice (reuse_choice) with the extra
+// rollout's priced rows loaded beside the totals and the two K-ranked candidates' priced rows
+// beside the t-chains, then writes the chosen candidate's params, noise, control and state rows
+// (k_noise_rows<REUSE>'s rows, computed ahead by the same expressions).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_reuse_pick(NoiseArgs a, ReuseArgs ra)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_rp[];
+    if (a.stop && *a.stop) return;
+    const int J = a.J, N = a.N, JN = J * N, K = ra.K;
+    const int r = a.row_begin + blockIdx.x, rr = r - ra.K_gen;
+    const size_t row = (size_t)r * JN;
+    const int tid = threadIdx.x;
+    STAMP(0);
+    double* costs = lds_rp;                      // [K rounded up to 8]
+    double* stage = costs + ((K + 7) & ~7);      // [J + 1][N]
+    constexpr int kL = 2048 / BLOCK;             // the rows' first pass in registers
+    double xp[kL], xn[kL], xc[kL], ap[kL], an[kL], ac[kL], bp[kL], bn[kL], bc[kL];
+    double sx = 0.0, sa, sb;
+    const int ti = min(tid, N - 1);
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+    auto live = [&](int u) { return wbase + u * BLOCK < JN; };
+    const size_t xo = (size_t)K * JN;
+    int selA, selB;
+    const int src = reuse_choice<BLOCK>(
+        ra, J, N, rr, costs, stage, tid,
+        [&]() {
+            if (ra.with_extra) {
+#pragma unroll
+                for (int u = 0; u < kL; ++u) {
+                    const size_t idx = xo + min(tid + u * BLOCK, JN - 1);
+                    if (live(u)) {
+                        xp[u] = ra.spec_params[idx];
+                        xn[u] = ra.spec_noise[idx];
+                        xc[u] = ra.spec_ctl[idx];
+                    }
+                }
+                sx = ra.x_state[ti];
+            }
+        },
+        [&](int A, int B) {
+            selA = A;
+            selB = B;
+            const size_t oa = (size_t)A * JN, ob = (size_t)B * JN;
+#pragma unroll
+            for (int u = 0; u < kL; ++u) {
+                const int idx = min(tid + u * BLOCK, JN - 1);
+                if (live(u)) {
+                    ap[u] = ra.spec_params[oa + idx];
+                    an[u] = ra.spec_noise[oa + idx];
+                    ac[u] = ra.spec_ctl[oa + idx];
+                    bp[u] = ra.spec_params[ob + idx];
+                    bn[u] = ra.spec_noise[ob + idx];
+                    bc[u] = ra.spec_ctl[ob + idx];
+                }
+            }
+            sa = ra.src_state[(size_t)A * N + ti];
+            sb = ra.src_state[(size_t)B * N + ti];
+        });
+    const int pick = src == selA ? 0 : (src == selB ? 1 : 2);
+    if (tid < N) ra.state[(size_t)r * N + tid] = pick == 0 ? sa : (pick == 1 ? sb : sx);
+#pragma unroll
+    for (int u = 0; u < kL; ++u) {
+        const int idx = tid + u * BLOCK;
+        if (idx < JN) {
+            a.params[row + idx] = pick == 0 ? ap[u] : (pick == 1 ? bp[u] : xp[u]);
+            a.noise[row + idx] = pick == 0 ? an[u] : (pick == 1 ? bn[u] : xn[u]);
+            a.control[row + idx] = pick == 0 ? ac[u] : (pick == 1 ? bc[u] : xc[u]);
+        }
+    }
+    // rows longer than the register pass, and state rows longer than the block: copied
+    const size_t os = (size_t)src * JN;
+    for (int idx = tid + kL * BLOCK; idx < JN; idx += BLOCK) {
+        a.params[row + idx] = ra.spec_params[os + idx];
+        a.noise[row + idx] = ra.spec_noise[os + idx];
+        a.control[row + idx] = ra.spec_ctl[os + idx];
+    }
+    const double* ssrc = src < K ? ra.src_state + (size_t)src * N : ra.x_state;
+    for (int i = tid + BLOCK; i < N; i += BLOCK) ra.state[(size_t)r * N + i] = ssrc[i];
+    STAMP(5);
+}
+
 namespace {
 
 size_t noise_rows_lds(const NoiseArgs& a, int n)
@@ -426,6 +538,31 @@ void launch_reuse_rows(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s)
     const int rows = a.K_loc - a.row_begin;
     if (rows <= 0) return;
     launch_noise_rows<true>(a, ra, rows, noise_rows_lds(a, ra.K + 8), s);   // the totals + inf padding
+}
+
+size_t price_candidate_lds_bytes(int J, int N)
+{
+    return ((size_t)(N + kBandBatch) * noise_jp(J) + 2 * (size_t)J * (N + 12) + (size_t)J * N) * sizeof(double);
+}
+
+namespace {
+size_t reuse_pick_lds(const NoiseArgs& a, int K)
+{
+    return ((size_t)((K + 7) & ~7) + (size_t)(a.J + 1) * a.N) * sizeof(double);
+}
+}  // namespace
+
+bool launch_reuse_pick_ok(const NoiseArgs& a, int K, int Kr)
+{
+    return launch_reuse_rows_ok(a, K, Kr) && price_candidate_lds_bytes(a.J, a.N) <= kRolloutLdsMax &&
+           reuse_pick_lds(a, K) <= 64 * 1024;
+}
+
+void launch_reuse_pick(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s)
+{
+    const int rows = a.K_loc - a.row_begin;
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_reuse_pick<512>, dim3(rows), dim3(512), reuse_pick_lds(a, ra.K), s, a, ra);
 }
 
 STOMP_STAMP_ACCESSORS(noise)

@@ -225,6 +225,15 @@ struct CostArgs {
     const double* tot_state;
     const double* tot_control;
     double* tot_out;
+    // blocks after the totals ones (one device, reuse; launch_reuse_pick): every reuse candidate
+    // re-based on nz.theta and priced ahead of the ranking, as the reused rows' kernel would price
+    // it (price_candidate): c < spec_rows - 1 the previous row c (spec_src), c = spec_rows - 1
+    // the extra rollout (params theta), into spec_params / spec_noise / spec_ctl row c
+    int spec_rows;
+    const double* spec_src;     // [K][J][N]
+    double* spec_params;        // [K + 1][J][N]
+    double* spec_noise;
+    double* spec_ctl;
 };
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };
@@ -318,9 +327,25 @@ struct ReuseArgs {
     const double* x_state;
     const double* x_control;
     double* state;              // this iteration's state rows (rows K_gen.. written)
+    // launch_reuse_pick: the candidates priced by the rollout launch (CostArgs::spec_*, row K the
+    // extra rollout)
+    const double* spec_params;
+    const double* spec_noise;
+    const double* spec_ctl;
 };
 bool launch_reuse_rows_ok(const NoiseArgs& a, int K, int Kr);
 void launch_reuse_rows(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s);
+// The reuse step when the rollout launch priced every candidate ahead (CostArgs::spec_*): one
+// workgroup per reused row ranks the candidates (the extra rollout's total made here) and copies
+// the chosen candidate's priced params / noise / control rows and its state row.  LDS of one
+// pricing block of the rollout launch: price_candidate_lds_bytes.
+bool launch_reuse_pick_ok(const NoiseArgs& a, int K, int Kr);
+// pieces per rollout of a split rollout launch of nro rollouts and extra_blocks pregen / totals /
+// pricing blocks (spec: pricing blocks present), 0 when the launch does not split; only a split
+// launch carries pricing blocks
+int rollout_split_pieces(const DevModel& m, int nro, int extra_blocks, bool spec);
+void launch_reuse_pick(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s);
+size_t price_candidate_lds_bytes(int J, int N);
 // the theta-independent part of generateRollouts + computeProjectedNoise for rows [0, rows):
 // normals, eps = sigma L z and M eps into a.pre_eps / a.pre_meps (run ahead on a side stream)
 void launch_pregen(const NoiseArgs& a, int rows, hipStream_t s);

@@ -457,6 +457,69 @@ __device__ __forceinline__ void rollout_control(const NoiseArgs& a, size_t row, 
     STAMP(63);
 }
 
+// One reuse candidate re-based on theta and priced (policy_improvement.cpp:208-224, then
+// computeProjectedNoise :473-482 and computeControlCosts): params p = psrc (theta itself when
+// psrc is null: the extra rollout), noise p - theta, x = p + M (p - theta) with M eps on the fp64
+// matrix cores, then rollout_control; the rows to out_params / out_noise / out_ctl.  The copy,
+// roundings and order of k_noise_rows<REUSE>.  The whole block calls it; lds:
+// (N + kBandBatch) JP + 2 J Nall + J N doubles.
+template <int BLOCK, int NG>
+__device__ __forceinline__ void price_candidate(const NoiseArgs& a, const double* psrc, double* out_params,
+                                                double* out_noise, double* out_ctl, double* lds, int tid)
+{
+    const int J = a.J, N = a.N, Nall = a.Nall, JP = noise_jp(J), NB = N + kBandBatch, JN = J * N;
+    double* eps = lds;            // [NB][JP], zero rows past N and zero columns past J
+    double* xs = eps + NB * JP;   // [J][Nall]
+    double* cs = xs + J * Nall;   // [J][Nall]
+    double* prm = cs + J * Nall;  // [J][N]
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+    constexpr int kLoads = 2048 / BLOCK;
+    for (int i0 = 0; i0 < JN; i0 += kLoads * BLOCK) {
+        double vt[kLoads], vp[kLoads];
+#pragma unroll
+        for (int u = 0; u < kLoads; ++u) {
+            if (i0 + wbase + u * BLOCK < JN) {   // wave-uniform: only the live loads
+                const int idx = min(i0 + tid + u * BLOCK, JN - 1);
+                vt[u] = a.theta[idx];
+                vp[u] = psrc ? psrc[idx] : vt[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kLoads; ++u) {
+            const int idx = i0 + tid + u * BLOCK;
+            if (idx < JN) {
+                const int d = idx / N, k = idx - d * N;
+                const double e = vp[u] - vt[u];
+                out_params[idx] = vp[u];
+                out_noise[idx] = e;
+                eps[k * JP + d] = e;
+                prm[idx] = vp[u];
+            }
+        }
+    }
+    for (int idx = tid; idx < NB * JP; idx += BLOCK) {
+        const int k = idx / JP, d = idx - k * JP;
+        if (k >= N || d >= J) eps[idx] = 0.0;
+    }
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int irow = 4 * ((lane >> 2) & 3) + (lane >> 4), jcol = lane & 3;
+    const int nti = (N + 15) >> 4;
+    const int mat_bytes = (N + kMatPadRows) * N * (int)sizeof(double);
+    const __amdgpu_buffer_rsrc_t rM = __builtin_amdgcn_make_buffer_rsrc((void*)a.MT, 0, mat_bytes, 0x00020000);
+    for (int ti = wv; ti < nti; ti += BLOCK / 64) {
+        double acc[NG];
+        mfma_tile<NG>(rM, N, 16 * ti, N, eps, JP, lane, acc);
+        const int i = 16 * ti + irow;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int d = 4 * g + jcol;
+            if (i < N && d < J) xs[d * Nall + i + 6] = prm[d * N + i] + acc[g];
+        }
+    }
+    rollout_control<BLOCK>(a, 0, xs, cs, tid, out_ctl);
+}
+
 // k_pregen's row, first half: normals (rollout_normals, already issued) and
 // eps = sigma_d (0 + L z), the same tiles and roundings as rollout_project_ng, written to
 // a.pre_eps and (layout [i][JP], for pregen_meps_ng) to the LDS buffer zB.  (M eps as a

@@ -173,6 +173,19 @@ def test_iterations_bitwise(K, Kr):
         _compare_iteration(o, e, it)
 
 
+@pytest.mark.parametrize("no_spec", ["0", "1"])
+@pytest.mark.parametrize("dof,K,Kr", [(7, 20, 10), (14, 16, 6), (7, 12, 11)])
+def test_reused_rows_priced_ahead_or_after_bitwise(monkeypatch, no_spec, dof, K, Kr):
+    # the reuse step on one device: every candidate priced by the rollout launch and the chosen
+    # one copied (k_reuse_pick), or (STOMP_DEBUG_NO_SPEC=1) the chosen row priced after the
+    # ranking (k_noise_rows<REUSE>); K_r = K - 1 reaches the lowest-ranked candidates
+    monkeypatch.setenv("STOMP_DEBUG_NO_SPEC", no_spec)
+    p = make(dof=dof, K=K, Kr=Kr)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    for it in range(1, 7):
+        _compare_iteration(o, e, it)
+
+
 def test_per_joint_noise_schedule_bitwise():
     # params.yaml:19-26 gives noise_stddev / noise_decay per joint (policy_improvement_loop.cpp:155-160)
     sig = [2.0, 1.5, 3.0, 0.5, 2.5, 1.0, 4.0]
