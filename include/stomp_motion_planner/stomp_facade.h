@@ -469,8 +469,18 @@ private:
                                 std::string& err) const;
     StompTrajectory* trajectory_;
     const StompParameters* parameters_;
-    stomp_engine_desc desc_{};          // the engine's descriptor (its tables are the caller's)
+    // the engine's descriptor, kept for createSibling: its tables point into the copies below,
+    // taken at construction (the caller may resize or reassign its vectors afterwards).  The
+    // distance field is the one exception: grid.data stays the caller's buffer, which must
+    // outlive the optimizer as the collision space does in the reference (StompOptimizer keeps
+    // its collision_space_ pointer, stomp_optimizer.cpp:61); a sibling uploads its own copy
+    stomp_engine_desc desc_{};
     Constraints constraints_;           // desc_.orientation_constraints points here
+    std::vector<stomp_segment> segments_;
+    std::vector<stomp_joint> joints_;
+    std::vector<stomp_sphere> spheres_;
+    std::vector<stomp_inertia> inertias_;
+    std::vector<double> noise_stddev_, noise_decay_, start_, goal_;
     stomp_engine* engine_ = nullptr;
     std::shared_ptr<Policy> policy_;
     int J_ = 0, N_ = 0;

@@ -57,6 +57,15 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
         error_ = "StompOptimizer: noise_stddev and noise_decay need one entry per joint";
         return;
     }
+    // the descriptor's tables: copies owned here (createSibling reads them any time later)
+    segments_ = robot_model->segments;
+    joints_ = robot_model->joints;
+    spheres_ = robot_model->collision_points;
+    inertias_ = robot_model->inertias;
+    noise_stddev_ = p.noise_stddev;
+    noise_decay_ = p.noise_decay;
+    start_ = trajectory->start;
+    goal_ = trajectory->goal;
     stomp_engine_desc d{};
     d.abi_version = STOMP_ENGINE_ABI_VERSION;
     d.num_joints = J_;
@@ -64,10 +73,10 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
     d.num_rollouts = p.num_rollouts;
     d.num_reused_rollouts = p.num_reused_rollouts;
     d.num_segments = (int32_t)robot_model->segments.size();
-    d.segments = robot_model->segments.data();
-    d.num_spheres = (int32_t)robot_model->collision_points.size();
-    d.spheres = robot_model->collision_points.data();
-    d.joints = robot_model->joints.data();
+    d.segments = segments_.data();
+    d.num_spheres = (int32_t)spheres_.size();
+    d.spheres = spheres_.data();
+    d.joints = joints_.data();
     d.grid = collision_space->grid;
     d.discretization = p.trajectory_discretization;
     d.smoothness_costs[0] = p.smoothness_cost_velocity;
@@ -78,11 +87,11 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
     d.obstacle_cost_weight = p.obstacle_cost_weight;
     d.constraint_cost_weight = p.constraint_cost_weight;
     d.torque_cost_weight = p.torque_cost_weight;
-    d.noise_stddev = p.noise_stddev.data();
-    d.noise_decay = p.noise_decay.data();
+    d.noise_stddev = noise_stddev_.data();
+    d.noise_decay = noise_decay_.data();
     d.use_cumulative_costs = p.use_cumulative_costs ? 1 : 0;
-    d.start = trajectory->start.data();
-    d.goal = trajectory->goal.data();
+    d.start = start_.data();
+    d.goal = goal_.data();
     d.seed = p.seed;
     d.max_iterations = p.max_iterations;
     d.max_iterations_after_collision_free = p.max_iterations_after_collision_free;
@@ -90,7 +99,7 @@ StompOptimizer::StompOptimizer(StompTrajectory* trajectory, const StompRobotMode
     d.stream = stream;
     d.rank = 0;
     d.world_size = 1;
-    d.inertias = robot_model->inertias.size() == robot_model->segments.size() ? robot_model->inertias.data() : nullptr;
+    d.inertias = inertias_.size() == segments_.size() ? inertias_.data() : nullptr;
     d.torque_root = robot_model->torque_root;
     d.torque_tip = robot_model->torque_tip;
     for (int k = 0; k < 3; ++k) d.gravity[k] = robot_model->gravity[k];

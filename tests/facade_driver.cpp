@@ -25,10 +25,12 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "stomp_motion_planner/stomp_facade.h"
@@ -716,6 +718,27 @@ int main(int argc, char** argv)
         std::ifstream f(argv[5]);
         f >> kr >> flip;
         if (!f) return 2;
+        // the caller's tables move after construction (same values, new storage; the old storage
+        // kept alive and overwritten): the engines made later for the PolicyImprovement
+        // (createSibling) must read the optimizer's own copies, not the caller's old buffers
+        std::vector<std::shared_ptr<void>> graveyard;
+        auto reseat = [&](auto& v) {
+            using V = std::decay_t<decltype(v)>;
+            V saved = v;
+            for (auto& x : v) std::memset((void*)&x, 0x7f, sizeof x);
+            auto old = std::make_shared<V>();
+            old->swap(v);
+            graveyard.push_back(old);
+            v = saved;
+        };
+        reseat(p.robot.segments);
+        reseat(p.robot.joints);
+        reseat(p.robot.collision_points);
+        reseat(p.robot.inertias);
+        reseat(p.params.noise_stddev);
+        reseat(p.params.noise_decay);
+        reseat(p.traj.start);
+        reseat(p.traj.goal);
         std::shared_ptr<Policy> policy;
         opt->getPolicy(policy);
         PolicyImprovement pi;
