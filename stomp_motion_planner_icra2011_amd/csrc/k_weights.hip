@@ -438,6 +438,73 @@ __global__ __launch_bounds__(BLOCK) void k_weights_rows_group(const WeightArgs* 
     weights_rows<BLOCK, TCW, EPT>(as[p], blockIdx.x - p * nt, nt, V);
 }
 
+// K_loc <= 64 (one canonical block), FUSED: one wave per flat column c = d N + t, lane r = rollout
+// r, and no LDS or barrier at all: S = state + control (or the cumulative row), min / max by
+// butterfly shuffles over the live lanes, P = exp(...) / (0.0 + sum_r exp), u = 0.0 + sum_r
+// eps P, both sums r ascending from 0.0 through readlanes (the one-block canonical order of
+// weights_rows, bit for bit).  Four columns per workgroup, grouped by XCD like the row tiles.
+__device__ __forceinline__ double readlane_f64(double x, int l)
+{
+    const long long b = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
+__global__ __launch_bounds__(256) void k_weights_wave(WeightArgs a)
+{
+    if (a.stop && *a.stop) return;
+    const int N = a.N, JN = a.J * N, K = a.K_loc;
+    const int nt = gridDim.x, bid = blockIdx.x;
+    const int x = bid & 7, q8 = nt >> 3, r8 = nt & 7;
+    const int tile = x * q8 + min(x, r8) + (bid >> 3);
+    const int c = __builtin_amdgcn_readfirstlane(tile * 4 + (int)(threadIdx.x >> 6));
+    if (c >= JN) return;   // the whole wave
+    const int lane = threadIdx.x & 63, t = c % N;
+    const bool live = lane < K;
+    const size_t r = (size_t)min(lane, K - 1);
+    const double nz = a.noise[r * JN + c];
+    double v;
+    if (a.cum) {
+        v = a.cum[r * JN + c];
+    } else {
+        const double st = a.state[r * N + t], ct = a.control[r * JN + c];
+        v = st + ct;
+    }
+    double mn = live ? v : __builtin_inf(), mx = live ? v : -__builtin_inf();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double omn = __shfl_xor(mn, off, 64), omx = __shfl_xor(mx, off, 64);
+        if (omn < mn) mn = omn;
+        if (omx > mx) mx = omx;
+    }
+    double den = mx - mn;
+    if (den < 1e-8) den = 1e-8;
+    const double e = det_exp(-10.0 * (v - mn) / den);
+    double s = 0.0;
+    for (int q0 = 0; q0 < K; q0 += 8) {
+        double b[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[q] = readlane_f64(e, min(q0 + q, K - 1));
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (q0 + q < K) s += b[q];
+    }
+    const double ps = 0.0 + s;   // the block partials summed in block order from 0.0
+    const double pn = e / ps;
+    const double w = nz * pn;
+    if (live) a.prob[r * JN + c] = pn;
+    double s2 = 0.0;
+    for (int q0 = 0; q0 < K; q0 += 8) {
+        double b[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[q] = readlane_f64(w, min(q0 + q, K - 1));
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (q0 + q < K) s2 += b[q];
+    }
+    if (lane == 0) a.u[c] = 0.0 + s2;
+}
+
 STOMP_STAMP_ACCESSORS(weights)
 
 // columns per workgroup of the column-tile kernel (k_weights, the fallback past the row tiles): as
@@ -476,6 +543,10 @@ static void launch_rows_t(const WeightArgs& a, hipStream_t s)
 void launch_weights(const WeightArgs& a, hipStream_t s)
 {
     const int K = a.K_loc;
+    if (a.mode == W_FUSED && K <= kSumBlock) {   // one canonical block: a wave per column
+        hipLaunchKernelGGL(k_weights_wave, dim3((a.J * a.N + 3) / 4), dim3(256), 0, s, a);
+        return;
+    }
     switch (rows_tcw(K)) {
     case 4:
         if (K <= 4 * 64) return launch_rows_t<256, 4, 4>(a, s);   // few rows: the wider tile only waits longer
