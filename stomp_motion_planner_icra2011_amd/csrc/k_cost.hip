@@ -55,7 +55,9 @@ constexpr int kWideBlock = ROLLOUT_WIDE_BLOCK;
 #define ROLLOUT_SPLIT_BLOCK 512
 #endif
 constexpr int kSplitBlock = ROLLOUT_SPLIT_BLOCK;
-constexpr int kSplitMaxDefault = 4;
+// pieces per rollout at most: cfg1 (11 rollouts) 25.6k it/s at 4, 26.4-26.9k at 5-7 (6: 26.7k, 25.1k
+// in the driver's window against 24.6k; profiles/ab/r5_split_pieces.txt)
+constexpr int kSplitMaxDefault = 6;
 template <int BLOCK>
 constexpr int rollout_min_waves()
 {
