@@ -262,7 +262,9 @@ def shard_why(e) -> str:
     """why the engine chose its K-sharded decomposition (measured at creation, maxima over ranks)"""
     i = e.shard_info
     if not i:
-        return ""
+        if os.environ.get("STOMP_SHARD_MODE"):
+            return ": requested by STOMP_SHARD_MODE"
+        return ": the only decomposition this shape allows (not measured)"
     g = i["t_gather"] + i["l_allgather_state"]
     p = i["t_partials"] + i["l_allreduce"] + 2 * i["l_allgather_partials"]
     return (f": measured gather {i['t_gather']:.1f} + all-gather {i['l_allgather_state']:.1f} = {g:.1f} us vs "
