@@ -77,6 +77,54 @@ __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const 
                fb[(3 * i + 2) * N + t] * pos[2] + fb[(9 + i) * N + t];
 }
 
+// The ordered fold of one waypoint's a values a[q * stride], q ascending over n: cum += a_q,
+// state += cum (stomp_optimizer.cpp:1099-1104), in the same order as a plain loop.  Whole batches
+// of 16 run unrolled.  The rest (n mod 16 terms) is loaded reversed (w[j] = a[rest - 1 - j]) and
+// entered by a switch on its length, so every register index is static: with an early exit
+// inside an unrolled loop the compiler indexed the batch's registers at run time
+// (s_set_gpr_idx_on / off around every term).
+__device__ __forceinline__ void fold_avalues(const double* av, int stride, int n, double& cum, double& state)
+{
+    int q0 = 0;
+    for (; q0 + 16 <= n; q0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = av[(q0 + q) * stride];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            cum += v[q];
+            state += cum;
+        }
+    }
+    const int rest = n - q0;
+    if (rest <= 0) return;
+    double w[15];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) w[j] = av[(q0 + max(rest - 1 - j, 0)) * stride];
+#define STOMP_FOLD_STEP(j) \
+    cum += w[j];           \
+    state += cum;
+    switch (rest) {
+    case 15: STOMP_FOLD_STEP(14) [[fallthrough]];
+    case 14: STOMP_FOLD_STEP(13) [[fallthrough]];
+    case 13: STOMP_FOLD_STEP(12) [[fallthrough]];
+    case 12: STOMP_FOLD_STEP(11) [[fallthrough]];
+    case 11: STOMP_FOLD_STEP(10) [[fallthrough]];
+    case 10: STOMP_FOLD_STEP(9) [[fallthrough]];
+    case 9: STOMP_FOLD_STEP(8) [[fallthrough]];
+    case 8: STOMP_FOLD_STEP(7) [[fallthrough]];
+    case 7: STOMP_FOLD_STEP(6) [[fallthrough]];
+    case 6: STOMP_FOLD_STEP(5) [[fallthrough]];
+    case 5: STOMP_FOLD_STEP(4) [[fallthrough]];
+    case 4: STOMP_FOLD_STEP(3) [[fallthrough]];
+    case 3: STOMP_FOLD_STEP(2) [[fallthrough]];
+    case 2: STOMP_FOLD_STEP(1) [[fallthrough]];
+    case 1: STOMP_FOLD_STEP(0) break;
+    default: break;
+    }
+#undef STOMP_FOLD_STEP
+}
+
 // |v| of sphere s at free waypoint t: the 7-tap velocity of its position (stomp_optimizer.cpp:683-698)
 // from the slot's frames in LDS, padding rows from the iteration-0 FK of start / goal
 __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* fb, const double* pad,
@@ -561,20 +609,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         }
         __syncthreads();   // every a value complete
         STAMP(12);
-        if (fk_lane) {
-            // fold in sphere order; the LDS reads go out 16 at a time
-            for (int q0 = 0; q0 < S; q0 += 16) {
-                double v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, S - 1) * N + t_own];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    if (q0 + q >= S) break;
-                    cum += v[q];
-                    state += cum;
-                }
-            }
-        }
+        if (fk_lane) fold_avalues(av + t_own, N, S, cum, state);   // in sphere order
         __builtin_amdgcn_s_setprio(2);
         STAMP(13);
     } else {
@@ -694,21 +729,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
         __builtin_amdgcn_s_setprio(3);
-        if (fk_lane) {
-            // fold in sphere order; the LDS reads go out 16 at a time
-            const int nsl = se - sb;
-            for (int q0 = 0; q0 < nsl; q0 += 16) {
-                double v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, nsl - 1) * N + t_own];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    if (q0 + q >= nsl) break;
-                    cum += v[q];
-                    state += cum;
-                }
-            }
-        }
+        if (fk_lane) fold_avalues(av + t_own, N, se - sb, cum, state);   // in sphere order
         // the program's control flow is uniform, so every lane has the same next op
         if constexpr (FK_OVERLAP) op = next_op;
         else op = fk_advance(op + 1);
@@ -1150,19 +1171,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
     double* to = extra ? a.x_total : (a.total_out ? a.total_out + e : nullptr);
     const bool combine = cfo || to;   // workgroup-uniform
     if (tid < Wo) {
-        // fold in sphere order
         double cum = 0.0, state = 0.0;
-        for (int q0 = 0; q0 < S; q0 += 16) {
-            double v[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = av[min(q0 + q, S - 1) * Wo + tid];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                if (q0 + q >= S) break;
-                cum += v[q];
-                state += cum;
-            }
-        }
+        fold_avalues(av + tid, Wo, S, cum, state);   // in sphere order
         so[t0 + tid] = m.w_obs * state + m.w_con * 0.0 + m.w_tq * 0.0;   // :1148-1151
         if (combine) __threadfence();   // release: the costs before this piece counts itself done
     }
