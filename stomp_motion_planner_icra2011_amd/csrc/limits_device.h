@@ -1,7 +1,6 @@
 // limits_device.h -- StompOptimizer::handleJointLimits (stomp_optimizer.cpp:562-616) for one wave
 // holding one joint's row of the trajectory in registers (lane l: waypoints l, l + 64, l + 128,
-// l + 192; N <= 256).  Shared by the rollout kernel (its joint-limit phase) and the update launch
-// that limits the next iteration's rows ahead of it (k_update_limits).
+// l + 192; N <= 256).  Used by the rollout kernel's joint-limit phase (k_cost.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,13 +21,15 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned x)
 }
 
 // the violated waypoint a pass corrects (wave-uniform), -1 when none is left: the largest
-// |amount| > 1e-6, the first index on ties (stomp_optimizer.cpp:574-593)
+// |amount| > 1e-6, the first index on ties (stomp_optimizer.cpp:574-593).  U: register slots per
+// lane (waypoints lane + 64 u, u < U; N <= 64 U)
+template <int U = 4>
 __device__ __forceinline__ int jl_argmax(const double* v, int N, int lane, double jmin, double jmax)
 {
     double cand = 0.0;   // absamt > 1e-6 > 0 marks a candidate
     int ci = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
         const int t = lane + 64 * u;
         if (t < N) {
             const double x = v[u];
@@ -56,12 +57,13 @@ __device__ __forceinline__ int jl_argmax(const double* v, int N, int lane, doubl
 
 // row += (amount / Q(cm, cm)) Q[:, cm] (stomp_optimizer.cpp:596-606); qv: this lane's entries of
 // column cm, qd = Q(cm, cm)
+template <int U = 4>
 __device__ __forceinline__ void jl_apply(double* v, int N, int lane, int cm, double jmin, double jmax,
                                          const double* qv, double qd)
 {
     double vu = v[0];
 #pragma unroll
-    for (int u = 1; u < 4; ++u)
+    for (int u = 1; u < U; ++u)
         if ((cm >> 6) == u) vu = v[u];   // uniform select
     const unsigned long long bits = (unsigned long long)__double_as_longlong(vu);
     const unsigned vlo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, cm & 63);
@@ -70,7 +72,7 @@ __device__ __forceinline__ void jl_apply(double* v, int N, int lane, int cm, dou
     const double amount = x > jmax ? jmax - x : jmin - x;
     const double mult = amount / qd;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < U; ++u)
         if (lane + 64 * u < N) v[u] += mult * qv[u];
 }
 

@@ -1,7 +1,6 @@
 // update_device.h -- one tile of theta += M u (policy_improvement.cpp:380, covariant_trajectory_policy
-// .cpp:318-323): 16 outputs of one joint.  Used by k_update (a launch of its own) and by the rollout
-// launch's update blocks (CostArgs::nupd, k_cost.hip), which apply the previous iteration's update
-// at the head of the next launch instead of in a launch of their own.
+// .cpp:318-323): 16 outputs of one joint.  Used by k_update, a launch of its own (the variant that
+// applied the update in blocks of the next rollout launch was measured and rejected).
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -61,6 +61,12 @@ def cost_label(i):
         return {61: "control terms (thread 0)", 62: "control terms barrier", 63: "control costs stored (t0)"}[i]
     if 100 <= i < 140:
         return f"FK op {i - 100}"
+    if 140 <= i < 160:
+        return f"JL pass {i - 140}: argmax, loads issued"
+    if 160 <= i < 180:
+        return f"JL pass {i - 160}: finished joints published"
+    if i == 180:
+        return "JL group end"
     if 40 <= i < 100:
         return f"slot {i - 40}: gathers issued (last round)"
     if 10 <= i < 40:
