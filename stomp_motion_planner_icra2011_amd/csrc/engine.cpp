@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -191,6 +192,19 @@ struct stomp_engine {
 #ifdef STOMP_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
+    // bounded waits over RCCL (sync_stream): the last collective posted (name, iteration, count),
+    // the deadline (STOMP_COMM_TIMEOUT_S, default 300 s), and the aborted communicator's message
+    const char* coll_name = "none";
+    int coll_it = -1;
+    long long coll_count = 0;
+    int cur_it = -1;
+    double comm_timeout_s = 300.0;
+    bool comm_aborted = false;
+    std::string comm_msg;
+    // STOMP_DEBUG_STALL_COLLECTIVE=n (tests): the n-th collective is withheld and the stream made
+    // to wait on h_stall instead (a rank that never posts it); released after the abort
+    long long stall_at = 0;
+    unsigned* h_stall = nullptr;
     // PolicyImprovement API (stomp_pi_*): the weight the control-cost rows were priced with,
     // improvePolicy's update (J x N)
     double pi_weight = 0.0;
@@ -241,6 +255,60 @@ struct DeviceGuard {
         hipError_t _st = (x);                                                                  \
         if (_st != hipSuccess)                                                                 \
             return fail((e), STOMP_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(_st));     \
+    } while (0)
+
+// hipStreamSynchronize of the engine stream, bounded when collectives are in it: over RCCL the
+// wait polls the stream and the communicator's asynchronous error, and after STOMP_COMM_TIMEOUT_S
+// seconds without completion (a rank that never posts its side of a collective, a mismatched
+// sequence) or on an RCCL error it aborts the communicator (ncclCommAbort also releases RCCL
+// kernels still waiting) and fails with STOMP_E_COMM naming the last collective posted.  Every
+// later call on the engine fails the same way.
+int sync_stream(stomp_engine* e)
+{
+#ifdef STOMP_WITH_RCCL
+    if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
+    if (e->comm) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (long long n = 0;; ++n) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) return 0;
+            if (q != hipErrorNotReady)
+                return fail(e, STOMP_E_DEVICE, "hipStreamQuery failed: %s", hipGetErrorString(q));
+            ncclResult_t ae = ncclSuccess;
+            const ncclResult_t qr = ncclCommGetAsyncError(e->comm, &ae);
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            const bool err = qr != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress);
+            if (err || el > e->comm_timeout_s) {
+                char buf[400];
+                if (err)
+                    snprintf(buf, sizeof buf, "rank %d: RCCL error (%s) with collectives in flight",
+                             e->rank, ncclGetErrorString(qr != ncclSuccess ? qr : ae));
+                else
+                    snprintf(buf, sizeof buf, "rank %d: collectives did not complete within %.1f s (STOMP_COMM_TIMEOUT_S)",
+                             e->rank, e->comm_timeout_s);
+                e->comm_msg = std::string(buf) + "; last collective posted: " + e->coll_name + " of iteration " +
+                              std::to_string(e->coll_it) + " (#" + std::to_string(e->coll_count) +
+                              "); communicator aborted";
+                ncclCommAbort(e->comm);
+                e->comm = nullptr;
+                e->comm_aborted = true;
+                if (e->h_stall) __atomic_store_n(e->h_stall, 1u, __ATOMIC_SEQ_CST);   // the test hook's wait
+                (void)hipStreamSynchronize(e->stream);   // the aborted collectives drain
+                (void)hipGetLastError();
+                return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
+            }
+            if (n > 2000) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+    }
+#endif
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+#define SYNC_TRY(e)                        \
+    do {                                   \
+        const int _rc = sync_stream(e);    \
+        if (_rc) return _rc;               \
     } while (0)
 
 template <class T>
@@ -439,8 +507,9 @@ void release(stomp_engine* e)
     if (e->h_total) hipHostFree(e->h_total);
     if (e->h_cf) hipHostFree(e->h_cf);
     if (e->h_track) hipHostFree(e->h_track);
+    if (e->h_stall) hipHostFree(e->h_stall);
 #ifdef STOMP_WITH_RCCL
-    if (e->comm) ncclCommDestroy(e->comm);
+    if (e->comm) ncclCommDestroy(e->comm);   // null once aborted (sync_stream)
 #endif
     if (e->ev_ready) hipEventDestroy(e->ev_ready);
     if (e->ev_done) hipEventDestroy(e->ev_done);
@@ -524,6 +593,24 @@ int flush_noiseless(stomp_engine* e)
         ncclResult_t _r = (x);                                                               \
         if (_r != ncclSuccess) return fail((e), STOMP_E_COMM, "%s: %s", #x, ncclGetErrorString(_r)); \
     } while (0)
+
+// a collective about to be posted on the engine stream: recorded for sync_stream's message;
+// returns 1 when the STOMP_DEBUG_STALL_COLLECTIVE hook withholds it (the stream then waits on
+// h_stall, as behind a rank that never posts it)
+int coll_post(stomp_engine* e, const char* name)
+{
+    e->coll_name = name;
+    e->coll_it = e->cur_it;
+    ++e->coll_count;
+    if (e->stall_at > 0 && e->coll_count == e->stall_at && e->h_stall) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, e->h_stall, 0) == hipSuccess &&
+            hipStreamWaitValue32(e->stream, dp, 1u, hipStreamWaitValueEq, 0xFFFFFFFFu) == hipSuccess)
+            return 1;
+        (void)hipGetLastError();
+    }
+    return 0;
+}
 #endif
 
 // all-gather of n doubles per rank, rank order, over the in-process group: publish the send
@@ -561,7 +648,9 @@ int local_gather(stomp_engine* e, const double* send, double* recv, size_t n)
 int exchange_max(stomp_engine* e, double* buf, size_t n)
 {
 #ifdef STOMP_WITH_RCCL
+    if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
     if (e->comm) {
+        if (coll_post(e, "all-reduce(max)")) return 0;
         NCCL_TRY(e, ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, e->comm, e->stream));
         return 0;
     }
@@ -578,7 +667,9 @@ int exchange_max(stomp_engine* e, double* buf, size_t n)
 int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
 {
 #ifdef STOMP_WITH_RCCL
+    if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
     if (e->comm) {
+        if (coll_post(e, "all-gather")) return 0;
         NCCL_TRY(e, ncclAllGather(send, recv, n, ncclFloat64, e->comm, e->stream));
         return 0;
     }
@@ -697,6 +788,8 @@ int begin_generate(stomp_engine* e)
 // the next iteration's rollout-cost launch (extra workgroup) or by flush_noiseless().
 int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
 {
+    if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
+    e->cur_it = it;
     const int member = it - 1;
     const bool fused = e->J <= 16;   // rollout_project: at most four 4-joint column groups
     // With fused noise the reuse step runs after the rollout launch: the generated rows go to
@@ -997,7 +1090,7 @@ int calibrate_shard_mode(stomp_engine* e)
     HIP_TRY(e, hipMemcpyAsync(e->d_mm, m, sizeof m, hipMemcpyHostToDevice, e->stream));
     if ((rc = exchange_max(e, e->d_mm, 5))) return rc;
     HIP_TRY(e, hipMemcpyAsync(m, e->d_mm, sizeof m, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     int32_t mode = 0;
     stomp_shard_decide(m, &mode);
     set_mode(mode == STOMP_SHARD_GATHER);
@@ -1014,6 +1107,7 @@ extern "C" {
 const char* stomp_last_error(void) { return g_last_error.c_str(); }
 
 const char* stomp_engine_last_error(const stomp_engine* e) { return e ? e->err.c_str() : g_last_error.c_str(); }
+// stomp_engine_source_hash: in the object _build.py generates at link time (build/source_hash.cpp)
 
 // The hinge potential's zero case and the collision test of StompCollisionSpace::
 // getCollisionPointPotentialGradient (stomp_collision_space.h:193-228) as thresholds on a voxel's
@@ -1603,6 +1697,16 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         CREATE_TRY(dev_alloc(e, &e->d_mm_all, (size_t)world * 2 * J * N));
     }
 #ifdef STOMP_WITH_RCCL
+    if (const char* to = std::getenv("STOMP_COMM_TIMEOUT_S")) {
+        const double v = std::atof(to);
+        if (v > 0.0) e->comm_timeout_s = v;
+    }
+    if (const char* st = std::getenv("STOMP_DEBUG_STALL_COLLECTIVE")) {
+        e->stall_at = std::atoll(st);
+        if (e->stall_at > 0 && hipHostMalloc((void**)&e->h_stall, sizeof(unsigned), hipHostMallocMapped) != hipSuccess)
+            CREATE_TRY(fail(e, STOMP_E_DEVICE, "hipHostMalloc (stall hook) failed"));
+        if (e->h_stall) *e->h_stall = 0u;
+    }
     if (world > 1 && !local_id) {
         ncclUniqueId id;
         std::memcpy(&id, d->comm_id, sizeof id);
@@ -1619,11 +1723,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         double* d_sig = nullptr;
         CREATE_TRY(dev_alloc(e, &d_sig, 12));
         double r[12];
+        e->coll_name = "decomposition check (all-reduce(max))";
         if (hipMemcpyAsync(d_sig, h, sizeof h, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
             ncclAllReduce(d_sig, d_sig, 12, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess ||
-            hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-            hipStreamSynchronize(e->stream) != hipSuccess)
+            hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "decomposition check across ranks failed"));
+        CREATE_TRY(sync_stream(e));   // bounded: a rank that never gets here fails the others
         for (int k = 0; k < 12; k += 2)
             if (r[k] != -r[k + 1])
                 CREATE_TRY(fail(e, STOMP_E_COMM, "ranks disagree on the K-sharded decomposition (gather, K, J, N, K_r, "
@@ -1660,7 +1765,7 @@ int stomp_engine_get_theta(stomp_engine* e, double* theta)
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
     HIP_TRY(e, hipMemcpyAsync(theta, e->d_theta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1670,7 +1775,7 @@ int stomp_engine_set_theta(stomp_engine* e, const double* theta)
     DeviceGuard dg(e->device);
     flush_noiseless(e);   // a pending noiseless rollout belongs to the theta being replaced
     HIP_TRY(e, hipMemcpyAsync(e->d_theta, theta, sizeof(double) * e->J * e->N, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1684,7 +1789,7 @@ int stomp_engine_iterate(stomp_engine* e, int32_t it, stomp_iter_out* out)
     HIP_TRY(e, hipMemcpyAsync(e->h_total, e->d_total, sizeof(double), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(e->h_cf, e->d_cf, 1, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipMemcpyAsync(e->h_cf + 1, e->d_cs, 1, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     if (out) {
         out->cost = *e->h_total;
         out->collision_free = e->h_cf[0];
@@ -1711,7 +1816,7 @@ int stomp_engine_synchronize(stomp_engine* e)
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
     flush_noiseless(e);
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1756,7 +1861,7 @@ int stomp_engine_eval(stomp_engine* e, const double* params, int32_t num, double
         HIP_TRY(e, hipMemcpyAsync(constraints_satisfied, e->d_eval_cs, num, hipMemcpyDeviceToHost, e->stream));
     if (traj_out)
         HIP_TRY(e, hipMemcpyAsync(traj_out, e->d_eval_traj, sizeof(double) * num * JN, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1819,7 +1924,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
     }
     if (!rc) rc = flush_noiseless(e);   // the last iteration's noiseless rollout and its bookkeeping
     e->tracking = false;
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     e->pool.push_back(ev[0]);
     e->pool.push_back(ev[1]);
     if (rc) return rc;
@@ -1834,7 +1939,7 @@ int stomp_engine_optimize(stomp_engine* e, stomp_stats* st, double* costs_per_it
         HIP_TRY(e, hipMemcpy(costs_per_it, e->d_opt_costs, sizeof(double) * t.iterations, hipMemcpyDeviceToHost));
     // later launches (iterate / run / eval) are not gated
     HIP_TRY(e, hipMemsetAsync(e->d_track, 0, sizeof(int), e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     stomp_stats s;
     s.iterations = t.iterations;
     s.success = t.success;
@@ -1862,7 +1967,7 @@ int stomp_engine_get_best_torques(stomp_engine* e, double* torques)
     launch_terms(e->tq_model, ta, e->stream);
     HIP_TRY(e, hipGetLastError());
     HIP_TRY(e, hipMemcpyAsync(torques, e->d_tq, sizeof(double) * e->N, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1894,7 +1999,7 @@ int stomp_pi_get_rollouts(stomp_engine* e, int32_t iteration, const double* nois
     if (rollouts)
         HIP_TRY(e, hipMemcpyAsync(rollouts, e->d_params, sizeof(double) * e->K_gen * e->J * e->N,
                                   hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     if (num_generated) *num_generated = e->K_gen;
     return 0;
 }
@@ -1922,7 +2027,7 @@ int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double cont
         std::vector<double> st((size_t)K * N), ct((size_t)K * J * N);
         HIP_TRY(e, hipMemcpyAsync(st.data(), e->d_state, sizeof(double) * st.size(), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(e, hipMemcpyAsync(ct.data(), e->d_control, sizeof(double) * ct.size(), hipMemcpyDeviceToHost, e->stream));
-        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        SYNC_TRY(e);
         for (int r = 0; r < K; ++r) {
             const double* sr = st.data() + (size_t)r * N;
             double c = sr[0];
@@ -1936,7 +2041,7 @@ int stomp_pi_set_rollout_costs(stomp_engine* e, const double* costs, double cont
             totals[r] = c;
         }
     }
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1966,7 +2071,7 @@ int stomp_pi_improve_policy(stomp_engine* e, double* updates)
     HIP_TRY(e, hipGetLastError());
     if (updates)
         HIP_TRY(e, hipMemcpyAsync(updates, e->d_delta, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -1976,7 +2081,7 @@ int stomp_pi_reset(stomp_engine* e)
 {
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     e->reused_next = false;
     e->extra_added = false;
     return 0;
@@ -1994,7 +2099,7 @@ int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* para
     std::vector<double> th(JN), nz(JN);
     flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(th.data(), e->d_theta, sizeof(double) * JN, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     for (size_t k = 0; k < JN; ++k) nz[k] = params[k] - th[k];
     HIP_TRY(e, hipMemcpyAsync(e->d_x_params, params, sizeof(double) * JN, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(e, hipMemcpyAsync(e->d_x_noise, nz.data(), sizeof(double) * JN, hipMemcpyHostToDevice, e->stream));
@@ -2007,7 +2112,7 @@ int stomp_pi_add_extra_rollouts(stomp_engine* e, int32_t num, const double* para
     xa.params = e->d_x_params; xa.noise = e->d_x_noise; xa.control = e->d_x_control;
     launch_noise(xa, e->stream);
     HIP_TRY(e, hipGetLastError());
-    HIP_TRY(e, hipStreamSynchronize(e->stream));   // nz is a pageable host buffer
+    SYNC_TRY(e);   // nz is a pageable host buffer
     e->extra_added = true;
     return 0;
 }
@@ -2018,7 +2123,7 @@ int stomp_engine_get_best_trajectory(stomp_engine* e, double* traj)
     DeviceGuard dg(e->device);
     flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_best_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -2028,7 +2133,7 @@ int stomp_engine_get_last_trajectory(stomp_engine* e, double* traj)
     DeviceGuard dg(e->device);
     flush_noiseless(e);
     HIP_TRY(e, hipMemcpyAsync(traj, e->d_last_traj, sizeof(double) * e->J * e->N, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -2059,7 +2164,7 @@ int stomp_engine_get_rollouts(stomp_engine* e, const char* which, double* out)
     }
     else return fail(e, STOMP_E_INVALID, "unknown rollout field '%s'", which);
     HIP_TRY(e, hipMemcpyAsync(out, src, n * sizeof(double), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 
@@ -2095,7 +2200,7 @@ int stomp_engine_get_pad_positions(stomp_engine* e, double* out)
     if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
     DeviceGuard dg(e->device);
     HIP_TRY(e, hipMemcpyAsync(out, e->d_pad_pos, sizeof(double) * 12 * e->S * 3, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    SYNC_TRY(e);
     return 0;
 }
 

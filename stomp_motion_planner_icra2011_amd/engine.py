@@ -92,7 +92,7 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_pi_reset", "stomp_sdf_build_objects",
             "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
             "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy", "stomp_engine_shard_mode",
-            "stomp_engine_shard_info", "stomp_shard_decide"]
+            "stomp_engine_shard_info", "stomp_shard_decide", "stomp_engine_source_hash"]
 
 _lib = None
 
@@ -102,13 +102,23 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or os.environ.get("STOMP_ENGINE_LIB") or _LIB_PATH
+    explicit = path or os.environ.get("STOMP_ENGINE_LIB")
+    path = explicit or _LIB_PATH
     if not os.path.exists(path):
         if os.path.exists(_build.HIPCC):
             _build.build()
         else:
             raise RuntimeError(f"STOMP HIP engine library missing: {path} (run __graft_entry__.build())")
+    if not explicit:
+        # the product library must be built from this checkout's sources (a variant named by
+        # STOMP_ENGINE_LIB is an experiment's build with its own defines)
+        built, want = _build.embedded_hash(path), _build.source_hash()
+        if built != want:
+            raise RuntimeError(f"stale STOMP engine library {path}: built from sources {built}, the checkout's "
+                               f"are {want} (run __graft_entry__.build())")
     l = C.CDLL(path)
+    l.stomp_engine_source_hash.restype = C.c_char_p
+    l.stomp_engine_source_hash.argtypes = []
     P, dp = C.c_void_p, C.POINTER(C.c_double)
     l.stomp_engine_create.argtypes = [C.POINTER(stomp_engine_desc), C.POINTER(C.c_void_p)]
     l.stomp_engine_destroy.argtypes = [P]

@@ -247,6 +247,33 @@ def test_sharded_weight_phases_through_rccl_bitwise(monkeypatch):
     np.testing.assert_array_equal(e.theta(), o.theta())
 
 
+def test_stuck_collective_fails_within_the_deadline(monkeypatch):
+    # A rank that never posts its side of a collective, modelled on a one-rank RCCL communicator:
+    # STOMP_DEBUG_STALL_COLLECTIVE=5 withholds the fifth collective (iteration 2's first
+    # all-gather of the sharded weights phases) and makes the stream wait behind it.  The bounded
+    # wait aborts the communicator after STOMP_COMM_TIMEOUT_S and fails with STOMP_E_COMM naming
+    # that collective; later calls fail the same way instead of hanging.
+    import time
+    monkeypatch.setenv("STOMP_DEBUG_SHARDED_MODES", "1")
+    monkeypatch.setenv("STOMP_DEBUG_RCCL_ONE_RANK", "1")
+    monkeypatch.setenv("STOMP_COMM_TIMEOUT_S", "2")
+    monkeypatch.setenv("STOMP_DEBUG_STALL_COLLECTIVE", "5")
+    p = make(K=128, Kr=0)
+    e = eng.Engine(p)
+    t0 = time.time()
+    with pytest.raises(RuntimeError) as ei:
+        e.run(1, 3)
+        e.synchronize()
+    dt = time.time() - t0
+    msg = str(ei.value)
+    assert "error -4" in msg and "did not complete within 2.0 s" in msg, msg
+    assert "last collective posted: all-gather of iteration 2 (#5)" in msg, msg
+    assert "communicator aborted" in msg, msg
+    assert dt < 20, dt
+    with pytest.raises(RuntimeError, match="communicator aborted"):
+        e.run(4, 1)
+
+
 def test_waypoints_200_dual_arm_bitwise():
     p = make(dof=14, waypoints=200, K=64)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
