@@ -93,12 +93,18 @@ def workload_name(args) -> str:
     return args.workload + (" (modified)" if args.custom else "")
 
 
+def loaded_hash() -> str:
+    """the source hash compiled into the engine library this process loaded (stomp_engine_source_hash):
+    the build that was timed, which a PMC summary must match"""
+    from stomp_motion_planner_icra2011_amd import engine as eng
+    return eng.load_library().stomp_engine_source_hash().decode()
+
+
 def pmc_summary(workload: str = "cfg2"):
     """The newest committed rocprofv3 PMC summary (tools/pmc_traffic.py) of this workload on one
     GPU and whether it was taken of this build (the engine's source hash).  Returns (summary or
     None, provenance dict)."""
-    from stomp_motion_planner_icra2011_amd import _build
-    here = _build.source_hash()
+    here = loaded_hash()
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*rollout_cost_traffic*.json"), recursive=True),
                    key=os.path.getmtime)
     newest = None
@@ -114,9 +120,10 @@ def pmc_summary(workload: str = "cfg2"):
         if newest is None:
             newest = (rel, d.get("source_hash"))
         if d.get("source_hash") == here:
-            return d, {"file": rel, "workload": workload, "source_hash": here, "matches_build": True}
+            return d, {"file": rel, "workload": workload, "source_hash": here, "loaded_library_hash": here,
+                       "matches_build": True}
     return None, {"file": newest[0] if newest else None, "workload": workload,
-                  "source_hash": newest[1] if newest else None, "build_source_hash": here, "matches_build": False,
+                  "source_hash": newest[1] if newest else None, "loaded_library_hash": here, "matches_build": False,
                   "note": "no PMC pass of this build and workload is committed: traffic and VALU counts are null"}
 
 
@@ -431,6 +438,9 @@ def main():
             os.environ["GPU_MAX_HW_QUEUES"] = str(want)
     dist = None
     if world > 1:
+        # a stuck or mismatched collective fails the run within a minute (the engine's bounded wait
+        # aborts the communicator and names the collective) instead of hanging it
+        os.environ.setdefault("STOMP_COMM_TIMEOUT_S", "60")
         import torch.distributed as dist  # CPU rendezvous only: the data path is RCCL inside the engine
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
@@ -582,4 +592,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except RuntimeError as ex:
+        # an engine failure (e.g. STOMP_E_COMM from the bounded collective wait): the message, a
+        # non-zero exit, no retry
+        print(f"bench.py rank {os.environ.get('RANK', '0')}: {ex}", file=sys.stderr)
+        sys.exit(3)

@@ -92,7 +92,13 @@ typedef struct stomp_grid {
     double origin[3];
     double resolution;
     const uint16_t* data;       /* host pointer, or device pointer if data_on_device */
-    int32_t data_on_device;     /* 1: engine uses the buffer in place (caller keeps it alive) */
+    int32_t data_on_device;     /* 1: engine reads the buffer (caller keeps it alive): in place
+                                 * for a field of at most 64 MiB; a larger one (e.g. 512^3) is
+                                 * copied once at creation into the engine's 4^3-brick layout
+                                 * (STOMP_SDF_LAYOUT=brick|linear overrides the size rule), so a
+                                 * caller that rebuilds the field in the same buffer (e.g. with
+                                 * stomp_sdf_build_objects between plans) calls
+                                 * stomp_engine_refresh_field afterwards */
 } stomp_grid;
 
 /* KDL::RigidBodyInertia(m, cog, Ic) of a segment, in the segment frame; Ic about the
@@ -193,6 +199,13 @@ const char* stomp_last_error(void);
  * whose hash is not the checkout's, and bench.py reports the hash of the library it timed. */
 const char* stomp_engine_source_hash(void);
 
+/* Re-reads the caller's device field (data_on_device = 1) after the caller rebuilt it in place:
+ * with the engine's bricked copy the copy is remade (ordered on the engine stream after the work
+ * already enqueued there; the caller orders its own rebuild before this call); with the field used
+ * in place, nothing to do.  A host field (data_on_device = 0) was uploaded at creation:
+ * STOMP_E_UNSUPPORTED. */
+int stomp_engine_refresh_field(stomp_engine* e);
+
 int stomp_engine_get_theta(stomp_engine* e, double* theta);
 int stomp_engine_set_theta(stomp_engine* e, const double* theta);
 
@@ -204,8 +217,8 @@ int stomp_engine_run(stomp_engine* e, int32_t first_iteration, int32_t count);
 /* synchronize, and every other call that waits for the engine's stream: with an RCCL communicator
  * (world_size > 1) the wait is bounded.  An RCCL error, or no completion within
  * STOMP_COMM_TIMEOUT_S seconds (default 300), aborts the communicator (ncclCommAbort) and returns
- * STOMP_E_COMM with a message naming the last collective posted (its kind, iteration and ordinal);
- * every later call on the engine returns the same. */
+ * STOMP_E_COMM with a message naming the first collective not complete and the last one posted
+ * (kind, iteration and ordinal of each); every later call on the engine returns the same. */
 int stomp_engine_synchronize(stomp_engine* e);
 
 /* Batched Task::execute: params E x J x N, costs E x N, collision_free E,

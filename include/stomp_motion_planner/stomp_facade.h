@@ -285,6 +285,10 @@ public:
         detail::from_vecs(parameters, p);
         Vector c;
         if (!execute(p, c, iteration_number)) return false;
+        // task.h:70 takes parameters by non-const reference and the loop keeps what execute left
+        // there as the extra rollout (policy_improvement_loop.cpp:182-190): a plugin's in-place
+        // edits come back
+        parameters = detail::to_vecs(p);
         costs = detail::to_vec(c);
         return true;
     }

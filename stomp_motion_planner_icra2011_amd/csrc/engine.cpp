@@ -153,7 +153,9 @@ struct stomp_engine {
     bool spec_on = false;
     int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
-    uint16_t* d_sdf = nullptr;   // d2 per voxel
+    uint16_t* d_sdf = nullptr;   // d2 per voxel (the engine's bricked copy when model.brick)
+    const uint16_t* d_sdf_caller = nullptr;   // the caller's device field (data_on_device), or null
+    int grid_n[3] = {0, 0, 0};
     int* d_pad_cf = nullptr;
     int pad_collision = 0;
     bool reused_next = false, extra_added = false;
@@ -205,6 +207,15 @@ struct stomp_engine {
     // to wait on h_stall instead (a rank that never posts it); released after the abort
     long long stall_at = 0;
     unsigned* h_stall = nullptr;
+    // an event behind each of the last kCollRing collectives: the message names the first one not
+    // complete (the stuck one), not only the last one posted
+    static constexpr int kCollRing = 32;
+    struct CollRec {
+        hipEvent_t ev = nullptr;
+        const char* name = "";
+        int it = -1;
+        long long n = 0;
+    } coll_ring[kCollRing];
     // PolicyImprovement API (stomp_pi_*): the weight the control-cost rows were priced with,
     // improvePolicy's update (J x N)
     double pi_weight = 0.0;
@@ -286,13 +297,24 @@ int sync_stream(stomp_engine* e)
                 else
                     snprintf(buf, sizeof buf, "rank %d: collectives did not complete within %.1f s (STOMP_COMM_TIMEOUT_S)",
                              e->rank, e->comm_timeout_s);
-                e->comm_msg = std::string(buf) + "; last collective posted: " + e->coll_name + " of iteration " +
-                              std::to_string(e->coll_it) + " (#" + std::to_string(e->coll_count) +
-                              "); communicator aborted";
+                std::string stuck = "unknown (older than the last 32)";
+                for (long long k = std::max(1LL, e->coll_count - stomp_engine::kCollRing + 1); k <= e->coll_count; ++k) {
+                    const auto& r = e->coll_ring[k % stomp_engine::kCollRing];
+                    if (r.n == k && r.ev && hipEventQuery(r.ev) == hipErrorNotReady) {
+                        stuck = std::string(r.name) + " of iteration " + std::to_string(r.it) + " (#" + std::to_string(k) + ")";
+                        break;
+                    }
+                }
+                (void)hipGetLastError();
+                e->comm_msg = std::string(buf) + "; first collective not complete: " + stuck + "; last posted: " +
+                              e->coll_name + " of iteration " + std::to_string(e->coll_it) + " (#" +
+                              std::to_string(e->coll_count) + "); communicator aborted";
+                // the test hook's wait first: its withheld collective's successors are queued behind
+                // it and have not started, so the abort would wait for them
+                if (e->h_stall) __atomic_store_n(e->h_stall, 1u, __ATOMIC_SEQ_CST);
                 ncclCommAbort(e->comm);
                 e->comm = nullptr;
                 e->comm_aborted = true;
-                if (e->h_stall) __atomic_store_n(e->h_stall, 1u, __ATOMIC_SEQ_CST);   // the test hook's wait
                 (void)hipStreamSynchronize(e->stream);   // the aborted collectives drain
                 (void)hipGetLastError();
                 return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
@@ -508,6 +530,8 @@ void release(stomp_engine* e)
     if (e->h_cf) hipHostFree(e->h_cf);
     if (e->h_track) hipHostFree(e->h_track);
     if (e->h_stall) hipHostFree(e->h_stall);
+    for (auto& r : e->coll_ring)
+        if (r.ev) hipEventDestroy(r.ev);
 #ifdef STOMP_WITH_RCCL
     if (e->comm) ncclCommDestroy(e->comm);   // null once aborted (sync_stream)
 #endif
@@ -611,6 +635,21 @@ int coll_post(stomp_engine* e, const char* name)
     }
     return 0;
 }
+
+// the event behind the collective coll_post just recorded (or withheld)
+void coll_mark(stomp_engine* e)
+{
+    auto& r = e->coll_ring[e->coll_count % stomp_engine::kCollRing];
+    if (!r.ev && hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+        r.ev = nullptr;
+        (void)hipGetLastError();
+        return;
+    }
+    r.name = e->coll_name;
+    r.it = e->coll_it;
+    r.n = e->coll_count;
+    (void)hipEventRecord(r.ev, e->stream);
+}
 #endif
 
 // all-gather of n doubles per rank, rank order, over the in-process group: publish the send
@@ -650,8 +689,9 @@ int exchange_max(stomp_engine* e, double* buf, size_t n)
 #ifdef STOMP_WITH_RCCL
     if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
     if (e->comm) {
-        if (coll_post(e, "all-reduce(max)")) return 0;
-        NCCL_TRY(e, ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, e->comm, e->stream));
+        if (!coll_post(e, "all-reduce(max)"))
+            NCCL_TRY(e, ncclAllReduce(buf, buf, n, ncclFloat64, ncclMax, e->comm, e->stream));
+        coll_mark(e);
         return 0;
     }
 #endif
@@ -669,8 +709,8 @@ int exchange_gather(stomp_engine* e, const double* send, double* recv, size_t n)
 #ifdef STOMP_WITH_RCCL
     if (e->comm_aborted) return fail(e, STOMP_E_COMM, "%s", e->comm_msg.c_str());
     if (e->comm) {
-        if (coll_post(e, "all-gather")) return 0;
-        NCCL_TRY(e, ncclAllGather(send, recv, n, ncclFloat64, e->comm, e->stream));
+        if (!coll_post(e, "all-gather")) NCCL_TRY(e, ncclAllGather(send, recv, n, ncclFloat64, e->comm, e->stream));
+        coll_mark(e);
         return 0;
     }
 #endif
@@ -990,6 +1030,30 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
 // The calibration launches leave no state the first iteration reads: theta is untouched, the pregen
 // rows are remade (pre_it stays -1), and every row buffer is rewritten by the iterations.
 // STOMP_DEBUG_SHARD_LATENCY_US=x adds x us to every measured collective (tests: both selections).
+// partials chosen after a calibration that ran in gather mode's layout: the row buffers drop from
+// K rows to the rank's K_loc (about world_size times less memory); nothing in them is read again
+// (every row is rewritten by the iterations, the pregen rows are remade)
+int shrink_rows(stomp_engine* e)
+{
+    const size_t JN = (size_t)e->J * e->N, KJN = (size_t)e->rows * JN;
+    auto re = [&](double*& p, size_t n) -> int {
+        if (!p) return 0;
+        HIP_TRY(e, hipStreamSynchronize(e->stream));   // the calibration launches used it
+        auto it = std::find(e->allocs.begin(), e->allocs.end(), (void*)p);
+        if (it != e->allocs.end()) {
+            hipFree(*it);
+            e->allocs.erase(it);
+        }
+        p = nullptr;
+        return dev_alloc(e, &p, n);
+    };
+    int rc = 0;
+    for (double** p : {&e->d_params, &e->d_noise, &e->d_control, &e->d_prob, &e->d_cum, &e->d_pre_eps[0],
+                       &e->d_pre_eps[1], &e->d_pre_meps[0], &e->d_pre_meps[1]})
+        if ((rc = re(*p, KJN))) return rc;
+    return re(e->d_state, (size_t)e->rows * e->N);
+}
+
 int calibrate_shard_mode(stomp_engine* e)
 {
     const int J = e->J, N = e->N;
@@ -1095,6 +1159,7 @@ int calibrate_shard_mode(stomp_engine* e)
     stomp_shard_decide(m, &mode);
     set_mode(mode == STOMP_SHARD_GATHER);
     if (e->gather) HIP_TRY(e, hipMemsetAsync(e->d_state, 0, sizeof(double) * e->rows * N, e->stream));
+    else if ((rc = shrink_rows(e))) return rc;
     e->shard_info[0] = mode;
     for (int k = 0; k < 5; ++k) e->shard_info[1 + k] = m[k];
     return 0;
@@ -1238,10 +1303,13 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             e->gather = true;
             e->K_loc = e->K / W;
         } else if (world > 1 && can) {
+            // requested (STOMP_SHARD_MODE), or, where nothing is measured (an in-process group without
+            // STOMP_DEBUG_CALIBRATE_LOCAL), gather while the K N state rows fit 1 MiB
             e->gather = sm ? std::strcmp(sm, "gather") == 0 : (size_t)e->K * e->N * sizeof(double) <= (1u << 20);
         }
-        // with both decompositions possible and none requested, the choice is measured at the end of
-        // creation (calibrate_shard_mode); until then gather mode's layout, which holds every row
+        // over RCCL, with both decompositions possible and none requested, the choice is measured at
+        // the end of creation (calibrate_shard_mode); until then gather mode's layout, which holds every
+        // row (shrink_rows gives the buffers back when partials wins)
         // (the in-process exchange group calibrates only on request, STOMP_DEBUG_CALIBRATE_LOCAL=1:
         // its ranks must then be created on host threads of their own, as the measurement exchanges)
         const char* cl = std::getenv("STOMP_DEBUG_CALIBRATE_LOCAL");
@@ -1342,8 +1410,10 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     CREATE_TRY(upload(e, &e->d_start, e->start.data(), e->start.size()));
     CREATE_TRY(upload(e, &e->d_goal, e->goal.data(), e->goal.size()));
     const size_t ncell = (size_t)d->grid.nx * d->grid.ny * d->grid.nz;
+    e->grid_n[0] = d->grid.nx; e->grid_n[1] = d->grid.ny; e->grid_n[2] = d->grid.nz;
     if (d->grid.data_on_device) {
         e->d_sdf = (uint16_t*)d->grid.data;
+        e->d_sdf_caller = d->grid.data;
     } else {
         CREATE_TRY(upload(e, &e->d_sdf, d->grid.data, ncell));
     }
@@ -1723,10 +1793,12 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
         double* d_sig = nullptr;
         CREATE_TRY(dev_alloc(e, &d_sig, 12));
         double r[12];
-        e->coll_name = "decomposition check (all-reduce(max))";
         if (hipMemcpyAsync(d_sig, h, sizeof h, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
-            ncclAllReduce(d_sig, d_sig, 12, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess ||
-            hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+            (!coll_post(e, "decomposition check (all-reduce(max))") &&
+             ncclAllReduce(d_sig, d_sig, 12, ncclFloat64, ncclMax, e->comm, e->stream) != ncclSuccess))
+            CREATE_TRY(fail(e, STOMP_E_COMM, "decomposition check across ranks failed"));
+        coll_mark(e);
+        if (hipMemcpyAsync(r, d_sig, sizeof r, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
             CREATE_TRY(fail(e, STOMP_E_COMM, "decomposition check across ranks failed"));
         CREATE_TRY(sync_stream(e));   // bounded: a rank that never gets here fails the others
         for (int k = 0; k < 12; k += 2)
@@ -1758,6 +1830,18 @@ void stomp_engine_destroy(stomp_engine* e)
     DeviceGuard dg(e->device);
     release(e);
     delete e;
+}
+
+int stomp_engine_refresh_field(stomp_engine* e)
+{
+    if (!e) return fail(nullptr, STOMP_E_INVALID, "null engine");
+    if (!e->d_sdf_caller)
+        return fail(e, STOMP_E_UNSUPPORTED, "the distance field was uploaded from the host at creation (data_on_device = 0)");
+    if (!e->model.brick) return 0;   // read in place
+    DeviceGuard dg(e->device);
+    launch_sdf_bricks(e->d_sdf_caller, e->d_sdf, e->grid_n[0], e->grid_n[1], e->grid_n[2], e->stream);
+    HIP_TRY(e, hipGetLastError());
+    return 0;
 }
 
 int stomp_engine_get_theta(stomp_engine* e, double* theta)

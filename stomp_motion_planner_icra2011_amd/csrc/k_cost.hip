@@ -65,28 +65,8 @@ constexpr int rollout_min_waves()
 }
 // spheres of one run a pair lane takes: run_max(N) / (BLOCK / N) <= 16 / 2 (N <= 128) or 8 / 1
 constexpr int kLaneSpheres = 8;
-// own waypoints of a wave in the velocities-in-the-pair-phase body (PV): 64 lanes less the
-// stencil's halo (one lane before, two after)
-constexpr int kPvOwn = 64 - 3;
 static_assert(kRunMaxSmall / 2 <= kLaneSpheres && kRunMaxLarge <= kLaneSpheres && kBlock >= 256,
               "a pair lane's spheres of one run must fit kLaneSpheres");
-}
-
-// x of lane - 1 / lane + 1 of the wave (wave_shr:1 / wave_shl:1 DPP moves, both halves of the
-// double); the lane at the wave's edge gets its own value (the caller's halo lanes)
-__device__ __forceinline__ double lane_prev(double x)
-{
-    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)b, (int)(unsigned)b, 0x138, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(b >> 32), (int)(unsigned)(b >> 32), 0x138, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-__device__ __forceinline__ double lane_next(double x)
-{
-    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)b, (int)(unsigned)b, 0x130, 0xF, 0xF, false);
-    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(b >> 32), (int)(unsigned)(b >> 32), 0x130, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
@@ -316,8 +296,7 @@ __device__ __forceinline__ void spec_block(const CostArgs& a, int c, double* lds
 // slot's gathers are in flight (the running frame then stays live across the pair phases); off,
 // they advance after the fold from the frame reloaded from fb (fewer live registers: the grouped
 // launch, which is throughput-bound and register-capped at three workgroups per CU)
-// PV: the slot loop prices the velocities in the pair phase (N <= 2 kPvOwn, BLOCK = 256)
-template <int BLOCK, bool BRICK, bool PHASED = false, bool FK_OVERLAP = true, bool PV = false>
+template <int BLOCK, bool BRICK, bool PHASED = false, bool FK_OVERLAP = true>
 __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -659,102 +638,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // re-publish the same frame
         const int sb = o.sph_begin, se = o.sph_end;
         const int ns = se - sb;
-        int next_op = op;
-        if constexpr (PV) {
-            // Velocities in the pair phase (N <= 2 kPvOwn): wave wv takes sphere group gq = wv / W
-            // of the run (W = 1 or 2 waves per sphere) and the waypoint window t = (wv % W) kPvOwn
-            // + lane - 1: lanes 1 .. kPvOwn own their waypoint, lanes 0, 62, 63 are the velocity
-            // stencil's halo (taps t - 1 .. t + 2, stomp_optimizer.cpp:683-698).  Every lane makes
-            // its sphere position (from the slot's frame, or the padding row's position past the
-            // ends) and issues its voxel gather; the taps come from the neighbouring lanes by
-            // cross-lane moves and |v| is made while the gathers are in flight.  When the voxels
-            // land, a = pot * |v| where the potential is non-zero (+0 elsewhere), straight into
-            // the a-value buffer: no pair list and no velocity phase.  The positions, the taps, the
-            // sums and the potential are the other bodies' expressions in their order, so the a
-            // values are bit-identical.
-            const int W = N <= kPvOwn ? 1 : 2;
-            const int Gs = NW / W;
-            const int gq = wv / W, tq = (wv - gq * W) * kPvOwn + lane - 1;
-            const bool inr = tq >= 0 && tq < N;
-            const bool own = lane >= 1 && lane <= kPvOwn && inr;
-            const int tc = min(max(tq, 0), N - 1);
-            const int prow = min(max(tq < 0 ? tq + 6 : tq - N + 6, 0), 11);   // padding row (t < 0 or t >= N)
-            unsigned dv[kLaneSpheres];
-            double spd[kLaneSpheres];
-            unsigned okm = 0;
-            {
-                double F[12];
-#pragma unroll
-                for (int k = 0; k < 12; ++k) F[k] = fb[k * N + tc];
-#pragma unroll
-                for (int u = 0; u < kLaneSpheres; ++u) {
-                    if (u * Gs >= ns) break;   // uniform
-                    const int q = min(gq + u * Gs, ns - 1);
-                    const double* pos = sph[sb + q].pos;
-                    double x[3];
-#pragma unroll
-                    for (int i = 0; i < 3; ++i)
-                        x[i] = F[3 * i] * pos[0] + F[3 * i + 1] * pos[1] + F[3 * i + 2] * pos[2] + F[9 + i];
-                    if (!inr) {
-                        const double* src = pad + (prow * S + sb + q) * 3;
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) x[c] = src[c];
-                    }
-                    bool ok;
-                    const unsigned idx = sdf_cell<BRICK>(m, x, ok);
-                    dv[u] = m.sdf[idx];
-                    okm |= (unsigned)ok << u;
-                    // taps t - 1, t, t + 1, t + 2 (kVelTap0 .. kVelTap1)
-                    double y[4][3];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        y[1][c] = x[c];
-                        y[0][c] = lane_prev(x[c]);
-                        y[2][c] = lane_next(x[c]);
-                        y[3][c] = lane_next(y[2][c]);
-                    }
-                    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-#pragma unroll
-                    for (int kk = kVelTap0; kk <= kVelTap1; ++kk) {
-                        const double c = m.vel_coef[kk];
-                        if (c == 0.0) continue;   // 0 * p adds a signed zero: |v| unchanged
-                        v0 += c * y[kk - kVelTap0][0];
-                        v1 += c * y[kk - kVelTap0][1];
-                        v2 += c * y[kk - kVelTap0][2];
-                    }
-                    spd[u] = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                }
-            }
-            STAMP(40 + run);
-            if constexpr (FK_OVERLAP) {
-                __builtin_amdgcn_s_setprio(3);
-                next_op = fk_advance(op + 1);
-                __builtin_amdgcn_s_setprio(2);
-            }
-#pragma unroll
-            for (int u = 0; u < kLaneSpheres; ++u) {
-                if (u * Gs >= ns) break;   // uniform
-                const int q = gq + u * Gs;
-                if (own && q < ns) {
-                    const DevSphere& sp = sph[sb + q];
-                    const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
-                    col |= d2 < sp.col_lim;
-                    double av_q = 0.0;   // a = pot * |v| is +0 exactly when pot == +0
-                    if (d2 < sp.zero_lim) av_q = potential(sp, sdf_metres(m, (unsigned)d2)) * spd[u];
-                    av[q * N + tq] = av_q;
-                }
-            }
-            if constexpr (!FK_OVERLAP) {
-                if (fk_lane) {
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) C.R[k] = fb[k * N + t_own];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) C.p[k] = fb[(9 + k) * N + t_own];
-                }
-            }
-            __syncthreads();   // the run's a values complete; fb free for the next slot
-            STAMP(11 + 4 * run);
-        } else {
         // lane (g, t) = (tid / N, tid % N): its frame column is read once (all 12 LDS reads in
         // flight) and serves spheres g, g + G, ... of the slot
         // Every sphere of the run this lane takes (at most kLaneSpheres: a run holds <= 16
@@ -788,6 +671,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         // while the gathers are in flight the FK lanes run the program on to the next sphere
         // segment (C in registers; fb keeps this slot's frame for the velocities, and the next
         // frame is published after the fold)
+        int next_op = op;
         if constexpr (FK_OVERLAP) {
             __builtin_amdgcn_s_setprio(3);
             next_op = fk_advance(op + 1);
@@ -844,7 +728,6 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         }
         __syncthreads();   // the slot's a values complete; fb free for the next slot
         STAMP(12 + 4 * run);
-        }
         __builtin_amdgcn_s_setprio(3);
         if (fk_lane) fold_avalues(av + t_own, N, se - sb, cum, state);   // in sphere order
         // the program's control flow is uniform, so every lane has the same next op
@@ -894,10 +777,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     BLOCK_END();
 }
 
-template <int BLOCK, bool BRICK, bool PV = false>
+template <int BLOCK, bool BRICK>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
-    rollout_body<BLOCK, BRICK, false, true, PV>(m, a, blockIdx.x);
+    rollout_body<BLOCK, BRICK>(m, a, blockIdx.x);
 }
 
 // the phased evaluation for launches whose rollouts run one per CU (LDS: rollout_lds phased)
@@ -1452,17 +1335,6 @@ size_t rollout_phased_lds_bytes(const DevModel& m)
     return dyn;
 }
 
-// the slot-loop launches take the velocities-in-the-pair-phase body (PV) when a sphere's waypoints
-// fit two waves' windows
-static bool rollout_pv(const DevModel& m)
-{
-#ifdef STOMP_NO_PV
-    return false;
-#else
-    return kBlock == 256 && m.N <= 2 * kPvOwn;
-#endif
-}
-
 size_t rollout_static_lds()
 {
     hipFuncAttributes attr;
@@ -1476,12 +1348,9 @@ size_t rollout_static_lds()
 int rollout_blocks_per_cu(size_t lds_total)
 {
     hipFuncAttributes attr;
-    int regs = 0;
-    // both slot-loop bodies (rollout_pv picks one per shape): the larger register count
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false>) == hipSuccess) regs = attr.numRegs;
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false, true>) == hipSuccess)
-        regs = std::max(regs, attr.numRegs);
-    if (regs <= 0) regs = 256;
+    int regs = 256;
+    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false>) == hipSuccess && attr.numRegs > 0)
+        regs = attr.numRegs;
     const int alloc = (regs + 7) / 8 * 8;
     int waves_per_simd = 512 / alloc;
     if (waves_per_simd > 8) waves_per_simd = 8;
@@ -1519,11 +1388,6 @@ static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
     if (kWideBlock != kBlock && nro <= m.cus) {
         if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock, BRICK>, lds);
         hipLaunchKernelGGL((k_rollout<kWideBlock, BRICK>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);
-        return;
-    }
-    if (rollout_pv(m)) {
-        if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK, true>, lds);
-        hipLaunchKernelGGL((k_rollout<kBlock, BRICK, true>), dim3(blocks), dim3(kBlock), lds, s, m, a);
         return;
     }
     if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK>, lds);

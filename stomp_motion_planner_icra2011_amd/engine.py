@@ -92,7 +92,8 @@ EXPORTED = ["stomp_engine_create", "stomp_engine_destroy", "stomp_engine_last_er
             "stomp_pi_improve_policy", "stomp_pi_add_extra_rollouts", "stomp_pi_reset", "stomp_sdf_build_objects",
             "stomp_stream_create", "stomp_stream_destroy", "stomp_group_create", "stomp_group_run",
             "stomp_group_synchronize", "stomp_group_last_error", "stomp_group_destroy", "stomp_engine_shard_mode",
-            "stomp_engine_shard_info", "stomp_shard_decide", "stomp_engine_source_hash"]
+            "stomp_engine_shard_info", "stomp_shard_decide", "stomp_engine_source_hash",
+            "stomp_engine_refresh_field"]
 
 _lib = None
 
@@ -126,6 +127,7 @@ def load_library(path: Optional[str] = None):
     l.stomp_engine_last_error.argtypes = [P]
     l.stomp_last_error.restype = C.c_char_p
     l.stomp_engine_get_theta.argtypes = [P, dp]
+    l.stomp_engine_refresh_field.argtypes = [P]
     l.stomp_engine_set_theta.argtypes = [P, dp]
     l.stomp_engine_iterate.argtypes = [P, C.c_int32, C.POINTER(stomp_iter_out)]
     l.stomp_engine_run.argtypes = [P, C.c_int32, C.c_int32]
@@ -364,6 +366,10 @@ class Engine:
 
     def synchronize(self):
         _check(load_library().stomp_engine_synchronize(self.h), self.h)
+
+    def refresh_field(self):
+        """stomp_engine_refresh_field: the caller rebuilt its device field in place."""
+        _check(load_library().stomp_engine_refresh_field(self.h), self.h)
 
     def execute(self, params, iteration_member: int = 1):
         prm = np.ascontiguousarray(params, np.float64)

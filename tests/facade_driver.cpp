@@ -471,8 +471,46 @@ private:
     std::shared_ptr<Policy> p_;
 };
 
+// a reference-signature plugin that edits its parameters in place (task.h:70 takes them by
+// non-const reference): clamps every value to [-1, 1] and prices the clamped rows
+class ClampingTask : public TaskT<EigenLikeVector, NodeHandleLike> {
+public:
+    bool initialize(NodeHandleLike&, int) override { return true; }
+    bool execute(std::vector<EigenLikeVector>& parameters, EigenLikeVector& costs, const int) override
+    {
+        costs.resize(parameters.empty() ? 0 : parameters[0].size());
+        for (auto& row : parameters)
+            for (long i = 0; i < row.size(); ++i) {
+                row(i) = std::min(1.0, std::max(-1.0, row(i)));
+                costs(i) += row(i);
+            }
+        return true;
+    }
+    bool getPolicy(std::shared_ptr<Policy>&) override { return false; }
+    bool setPolicy(const std::shared_ptr<Policy>) override { return false; }
+    bool getControlCostWeight(double& w) override { w = 0.0; return true; }
+};
+
 int main(int argc, char** argv)
 {
+    if (argc >= 2 && std::string(argv[1]) == "taskt_writeback") {
+        // TaskT::execute hands the plugin's in-place edits back through the facade's Task (no device)
+        ClampingTask t;
+        Task& base = t;
+        std::vector<VectorXd> prm = {{-2.0, 0.5, 3.0}, {0.25, -7.0, 1.0}};
+        VectorXd c;
+        if (!base.execute(prm, c, 1)) return 60;
+        const double want[2][3] = {{-1.0, 0.5, 1.0}, {0.25, -1.0, 1.0}};
+        for (int d = 0; d < 2; ++d)
+            for (int i = 0; i < 3; ++i)
+                if (prm[d][i] != want[d][i]) {
+                    std::cerr << "row " << d << " entry " << i << ": " << prm[d][i] << " expected " << want[d][i] << "\n";
+                    return 61;
+                }
+        if (c.size() != 3 || c[0] != -0.75 || c[1] != -0.5 || c[2] != 2.0) return 62;
+        std::cout << "taskt_writeback OK\n";
+        return 0;
+    }
     if (argc < 4) {
         std::cerr << "usage: facade_driver problem.txt sdf.bin validate|optimize|loop [out]\n";
         return 2;

@@ -176,6 +176,16 @@ def test_facade_host_policy_improvement_cpu(tmp_path):
     assert "pi_host_cpu OK" in r.stdout
 
 
+def test_facade_taskt_hands_back_in_place_edits(tmp_path):
+    # TaskT::execute converts the parameters for a reference-signature plugin and writes the
+    # plugin's in-place edits back (task.h:70: non-const reference; the loop keeps them as the
+    # extra rollout, policy_improvement_loop.cpp:182-190)
+    exe = fu.build_driver(str(tmp_path))
+    r = subprocess.run([exe, "taskt_writeback"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "taskt_writeback OK" in r.stdout
+
+
 def _theta_cost_rows(toks, J, N, iters, extra=0):
     pos, rows = 0, []
     for _ in range(iters):

@@ -122,6 +122,30 @@ def test_brick_layout_bitwise(monkeypatch, grid_n, K):
         assert bool(cf[r]) == ocf
 
 
+def test_refresh_field_after_an_in_place_rebuild(monkeypatch):
+    # a device field the engine copies into its bricked layout (the default past 64 MiB; forced
+    # here at 64^3): after the caller rebuilds its buffer in place, stomp_engine_refresh_field
+    # remakes the copy, so the engine plans against the new field -- bit for bit the oracle of
+    # the new scene.  Without the refresh the engine keeps the field it was created with.
+    monkeypatch.setenv("STOMP_SDF_LAYOUT", "brick")
+    shelf, empty = make(K=16), make(K=16)
+    empty.boxes, empty.cylinders = [], []
+    empty.sdf = pb.build_sdf(empty.grid, [], [])
+    buf = eng.DeviceBuffer(2 * 64 ** 3)
+    eng.sdf_build_device(shelf, buf.ptr)
+    e = eng.Engine(empty, sdf_device_ptr=buf.ptr)
+    stale = eng.Engine(empty, sdf_device_ptr=buf.ptr)
+    eng.sdf_build_device(empty, buf.ptr)     # the scene changed: the shelf and the pole are gone
+    e.refresh_field()
+    o_new, o_old = po.Oracle(empty), po.Oracle(shelf)
+    for it in range(1, 4):
+        _compare_iteration(o_new, e, it)
+        o_old.iterate(it)
+        stale.iterate(it)
+    np.testing.assert_array_equal(stale.theta(), o_old.theta())
+    assert not np.array_equal(e.theta(), stale.theta())
+
+
 def test_slot_loop_runs_between_other_calls_bitwise():
     # K + 1 > CUs (the slot-loop launches of cfg2), pipelined runs interleaved with get_theta,
     # iterate, execute and set_theta: the pending noiseless rollout and the pregen rows made ahead
@@ -174,11 +198,13 @@ def test_iterations_bitwise(K, Kr):
 
 
 @pytest.mark.parametrize("no_spec", ["0", "1"])
-@pytest.mark.parametrize("dof,K,Kr", [(7, 20, 10), (14, 16, 6), (7, 12, 11)])
+@pytest.mark.parametrize("dof,K,Kr", [(7, 20, 10), (14, 16, 6), (7, 12, 11), (7, 96, 40), (7, 130, 129)])
 def test_reused_rows_priced_ahead_or_after_bitwise(monkeypatch, no_spec, dof, K, Kr):
     # the reuse step on one device: every candidate priced by the rollout launch and the chosen
     # one copied (k_reuse_pick), or (STOMP_DEBUG_NO_SPEC=1) the chosen row priced after the
-    # ranking (k_noise_rows<REUSE>); K_r = K - 1 reaches the lowest-ranked candidates
+    # ranking (k_noise_rows<REUSE>); K_r = K - 1 reaches the lowest-ranked candidates; K > 64
+    # takes reuse_choice's ranking through the shared sel[] array (k_noise.hip), at K = 96 in the
+    # split launch with its pricing blocks, at K = 130 (131 rollouts: no split) in the slot loop
     monkeypatch.setenv("STOMP_DEBUG_NO_SPEC", no_spec)
     p = make(dof=dof, K=K, Kr=Kr)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
@@ -267,7 +293,7 @@ def test_stuck_collective_fails_within_the_deadline(monkeypatch):
     dt = time.time() - t0
     msg = str(ei.value)
     assert "error -4" in msg and "did not complete within 2.0 s" in msg, msg
-    assert "last collective posted: all-gather of iteration 2 (#5)" in msg, msg
+    assert "first collective not complete: all-gather of iteration 2 (#5)" in msg, msg
     assert "communicator aborted" in msg, msg
     assert dt < 20, dt
     with pytest.raises(RuntimeError, match="communicator aborted"):

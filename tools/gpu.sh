@@ -36,7 +36,7 @@ bench_to() {  # bench_to OUT LIMIT ARGS...
 case "$cmd" in
 tests)
   mkdir -p gpurun_out/t
-  timeout -k 10 900 python3 -u -m pytest ${@:-tests} -m gpu -x -v --timeout 300 --timeout-method thread --durations=15 > gpurun_out/t/tests.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest ${@:-tests} -m gpu -x -v --timeout 150 --timeout-method thread --durations=15 > gpurun_out/t/tests.log 2>&1
   rc=$?
   tail -30 gpurun_out/t/tests.log
   exit $rc ;;

@@ -83,7 +83,7 @@ def main():
                       "between the two.  KiB -> B; Infinity-Cache hits are counted (memory side of L2), so this is "
                       "L2-miss traffic, an upper bound on HBM bytes",
         "stage": stage[0] if stage else None,
-        "source_hash": _build.source_hash(),
+        "source_hash": _build.embedded_hash(_build.LIB),   # the library the PMC passes ran
         "hbm_bytes_per_launch": sum(kernels[k].get("hbm_bytes", 0.0) for k in stage),
         "valu_insts_per_launch": sum(kernels[k].get("SQ_INSTS_VALU", 0.0) for k in stage),
         "valu_issue_frac": kernels[stage[0]].get("valu_issue_frac") if stage else None,
