@@ -97,6 +97,7 @@ def lib():
         l.so_get_best_torques.argtypes = [P, dp]
         l.so_get_last_trajectory.argtypes = [P, dp]
         l.so_get_rollouts.argtypes = [P, C.c_char_p, dp]
+        l.so_reuse_log.argtypes = [P, C.POINTER(C.c_int), C.c_int]
         l.so_philox4x32.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         l.so_normals.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, dp]
         l.so_diff_rules.argtypes = [dp]
@@ -197,7 +198,8 @@ class Oracle:
     def __init__(self, problem, dense: bool = False, threads: int = 1, sum_block: int = 64, ref_arith: int = 0):
         """dense: the reference's dense N x N products (CPU baseline structure); ref_arith 1: the
         reference's written arithmetic order (non-fused L z / M eps, sequential rollout sums)
-        instead of the engine's contract; 2: also Eigen 2's two-lane packet VectorXd::sum()."""
+        instead of the engine's contract; 2: also Eigen 2's two-lane packet VectorXd::sum(); 3: also
+        the C library's exp / sin / cos / atan2 / asin where the reference calls them."""
         L = lib()
         p = problem
         self.problem = p
@@ -339,6 +341,15 @@ class Oracle:
         if lib().so_get_rollouts(self.h, which.encode(), _dp(out)) != 0:
             raise KeyError(which)
         return out
+
+    def reuse_log(self) -> np.ndarray:
+        """[rankings][num_reused_rollouts] candidate indices kept by every reuse ranking so far
+        (-1 = the extra rollout), in generateRollouts' order (policy_improvement.cpp:198-224)."""
+        kr = max(int(self.problem.params.num_reused_rollouts), 1)
+        n = lib().so_reuse_log(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        lib().so_reuse_log(self.h, out.ctypes.data_as(C.POINTER(C.c_int)), n)
+        return out[:n].reshape(-1, kr)
 
     def sphere_positions(self, q) -> np.ndarray:
         qq = np.ascontiguousarray(q, np.float64)

@@ -20,6 +20,13 @@
  * cfg.ref_arith = 2 also sums VectorXd::sum() (Rollout::getCost, policy_improvement.cpp:149-156;
  * last_trajectory_cost_ = costs.sum(), stomp_optimizer.cpp:1155) as Eigen 2's SSE2 packet
  * reduction would: two interleaved lanes, then their sum (vec_sum).
+ * cfg.ref_arith = 3 also calls the C library's elementary functions where the reference does,
+ * instead of the deterministic dmath.h restatements the engine shares: exp in the rollout
+ * probabilities (policy_improvement.cpp:356, std::exp), sin / cos in KDL Rotation::Rot2
+ * (treefksolverjointposaxis_partial.cpp:125 -> KDL frames.inl), atan2 / asin / sin / cos in
+ * btMatrix3x3::getEulerYPR (constraint_evaluator.cpp:98).  The normals stay the shared Philox +
+ * Box-Muller draws (the reference's boost stream cannot be reproduced), so the modes differ in
+ * the arithmetic alone.
  * tests/test_reference_order.py measures how far the engine contract drifts from them on the
  * north-star quantity (best_group_trajectory_) and on the discrete decisions.
  */
@@ -67,6 +74,9 @@ struct so_problem {
     double *x_params, *x_noise, *x_nproj, *x_ctrl, *x_state;   /* the one extra rollout */
     double *tmp_params, *tmp_noise, *tmp_nproj, *tmp_ctrl, *tmp_prob, *tmp_state; /* reused_rollouts_ */
     int reused_next, extra_added, K_gen;
+    /* the reuse decisions of every ranking so far: Kr candidate indices each (-1 = the extra
+     * rollout), in the order generateRollouts kept them (policy_improvement.cpp:198-224) */
+    int *rank_log, rank_n, rank_cap;
     /* optimizer state */
     double* last_traj;     /* J x N (free block of group_trajectory_ after the last execute) */
     double last_cost;
@@ -205,10 +215,16 @@ double so_asin(double x) { return dm_asin(x); }
  * orocos KDL (3rd party, reached from treefksolverjointposaxis_partial.cpp:125). */
 typedef struct { double R[9]; double p[3]; } frame_t;
 
-static void rot2(const double* a, double angle, double* R)
+/* libm: the C library's sin / cos (ref_arith 3, as KDL calls them) instead of dm_sincos */
+static void rot2(const double* a, double angle, double* R, int libm)
 {
     double st, ct;
-    dm_sincos(angle, &st, &ct);
+    if (libm) {
+        st = sin(angle);
+        ct = cos(angle);
+    } else {
+        dm_sincos(angle, &st, &ct);
+    }
     double vt = 1.0 - ct;
     double m_vt_0 = vt * a[0], m_vt_1 = vt * a[1], m_vt_2 = vt * a[2];
     double m_st_0 = a[0] * st, m_st_1 = a[1] * st, m_st_2 = a[2] * st;
@@ -247,13 +263,13 @@ static int so_rot_identity(const double* r)
 }
 
 /* segment pose(q) composed onto the parent frame */
-static void segment_frame(const so_segment* s, const frame_t* parent, double q, frame_t* out)
+static void segment_frame(const so_segment* s, const frame_t* parent, double q, frame_t* out, int libm)
 {
     frame_t pose;
     const int ident = so_rot_identity(s->rot);
     if (s->q_index >= 0) {
         double Rq[9];
-        rot2(s->axis, q, Rq);
+        rot2(s->axis, q, Rq, libm);
         if (ident) memcpy(pose.R, Rq, sizeof pose.R);
         else rotmul(s->rot, Rq, pose.R);
     } else {
@@ -278,7 +294,7 @@ static void fk_spheres(const so_problem* P, const double* q, frame_t* frames, do
     for (int s = 0; s < P->nseg; ++s) {
         const so_segment* sg = &P->segs[s];
         double qv = sg->q_index >= 0 ? q[sg->q_index] : 0.0;
-        segment_frame(sg, sg->parent >= 0 ? &frames[sg->parent] : NULL, qv, &frames[s]);
+        segment_frame(sg, sg->parent >= 0 ? &frames[sg->parent] : NULL, qv, &frames[s], P->cfg.ref_arith >= 3);
     }
     for (int j = 0; j < P->S; ++j)   /* stomp_collision_point.h:138-141 */
         frame_apply(&frames[P->sph[j].segment], P->sph[j].pos, pos + 3 * j);
@@ -401,7 +417,7 @@ int so_inverse_dynamics(const so_problem* P, const double* q, const double* qd, 
         double* R = Rs[i];
         if (j >= 0) {
             double Rq[9];
-            rot2(sg->axis, qv, Rq);
+            rot2(sg->axis, qv, Rq, P->cfg.ref_arith >= 3);
             if (so_rot_identity(sg->rot)) memcpy(R, Rq, sizeof(double) * 9);
             else rotmul(sg->rot, Rq, R);
         } else {
@@ -482,6 +498,7 @@ static double torque_cost_at(const so_problem* P, const double* traj /* Nall x J
  *     (bullet LinearMath with BT_USE_DOUBLE_PRECISION, as built by ROS). */
 struct oc_eval {
     int seg, body_fixed;
+    int libm;              /* ref_arith 3: the C library's atan2 / asin / sin / cos */
     double ninv[9];        /* nominal_orientation_inverse_ */
     double rw, pw, yw;     /* roll/pitch/yaw weights (0 when the tolerance is >= pi) */
     double tol[3];         /* absolute roll / pitch / yaw tolerance */
@@ -548,12 +565,12 @@ static void kdl_get_quaternion(const double* R, double* x, double* y, double* z,
 }
 
 /* btMatrix3x3::getRPY -> getEulerYPR(yaw, pitch, roll, 1) */
-static void bt_get_rpy(const double* M, double* roll, double* pitch, double* yaw)
+static void bt_get_rpy(const double* M, double* roll, double* pitch, double* yaw, int libm)
 {
     const double pi = 3.1415926535897932384626433832795029;
     if (fabs(M[6]) >= 1.0) {
         *yaw = 0.0;
-        const double delta = dm_atan2(M[0], M[2]);
+        const double delta = libm ? atan2(M[0], M[2]) : dm_atan2(M[0], M[2]);
         if (M[6] > 0.0) {
             *pitch = pi / 2.0;
             *roll = *pitch + delta;
@@ -565,11 +582,17 @@ static void bt_get_rpy(const double* M, double* roll, double* pitch, double* yaw
         double a = M[6];   /* btAsin clamps to [-1, 1] */
         if (a < -1.0) a = -1.0;
         if (a > 1.0) a = 1.0;
-        *pitch = -dm_asin(a);
+        *pitch = -(libm ? asin(a) : dm_asin(a));
         double sp, cp;
-        dm_sincos(*pitch, &sp, &cp);
-        *roll = dm_atan2(M[7] / cp, M[8] / cp);
-        *yaw = dm_atan2(M[3] / cp, M[0] / cp);
+        if (libm) {
+            sp = sin(*pitch);
+            cp = cos(*pitch);
+        } else {
+            dm_sincos(*pitch, &sp, &cp);
+        }
+        (void)sp;
+        *roll = libm ? atan2(M[7] / cp, M[8] / cp) : dm_atan2(M[7] / cp, M[8] / cp);
+        *yaw = libm ? atan2(M[3] / cp, M[0] / cp) : dm_atan2(M[3] / cp, M[0] / cp);
     }
 }
 
@@ -612,7 +635,7 @@ static int oc_cost(const struct oc_eval* o, const double* R, double* cost)
     bt_from_quat(x, y, z, w, M);
     if (!o->body_fixed) bt_mul(M, o->ninv, res);
     else bt_mul(o->ninv, M, res);
-    bt_get_rpy(res, &roll, &pitch, &yaw);
+    bt_get_rpy(res, &roll, &pitch, &yaw, o->libm);
     roll = fabs(roll);
     pitch = fabs(pitch);
     yaw = fabs(yaw);
@@ -689,6 +712,7 @@ void so_destroy(so_problem* P)
     free(P->tmp_state);
     free(P->last_traj); free(P->best_traj);
     free(P->chain); free(P->rb_m); free(P->rb_h); free(P->rb_I); free(P->oc);
+    free(P->rank_log);
     free((void*)P->cfg.noise_stddev); free((void*)P->cfg.noise_decay);
     free((void*)P->cfg.start); free((void*)P->cfg.goal);
     free(P);
@@ -808,6 +832,7 @@ so_problem* so_create(const so_config* cfg)
             return NULL;
         }
         oc_init(&cfg->orientation_constraints[c], &P->oc[c]);
+        P->oc[c].libm = cfg->ref_arith >= 3;
     }
     P->cfg.orientation_constraints = NULL;
 
@@ -1240,7 +1265,7 @@ static void matvec(const double* A, int n, const double* x, double* y, int lower
  * lane 1, then the odd last element); otherwise index order. */
 static double vec_sum(const so_problem* P, const double* x, int n)
 {
-    if (P->cfg.ref_arith == 2 && n >= 2) {
+    if (P->cfg.ref_arith >= 2 && n >= 2) {
         double l0 = x[0], l1 = x[1];
         int i = 2;
         for (; i + 1 < n; i += 2) {
@@ -1327,6 +1352,17 @@ static void generate_rollouts(so_problem* P, int iteration_number, const double*
             P->extra_added = 0;
         }
         qsort(v, (size_t)n, sizeof(cost_idx), cmp_cost_idx);
+        if (P->rank_n + Kr > P->rank_cap) {
+            int cap = P->rank_cap ? 2 * P->rank_cap : 64 * (Kr > 0 ? Kr : 1);
+            while (cap < P->rank_n + Kr) cap *= 2;
+            int* nl = (int*)realloc(P->rank_log, sizeof(int) * (size_t)cap);
+            if (nl) {
+                P->rank_log = nl;
+                P->rank_cap = cap;
+            }
+        }
+        if (P->rank_n + Kr <= P->rank_cap)
+            for (int r = 0; r < Kr; ++r) P->rank_log[P->rank_n++] = v[r].idx;
         for (int r = 0; r < Kr; ++r) copy_rollout_out(P, v[r].idx, r);
         for (int r = 0; r < Kr; ++r) {
             int dst = P->K_gen + r;
@@ -1460,7 +1496,8 @@ int so_iterate(so_problem* P, int iteration_number, so_iter_out* out)
                 double denom = mx - mn;
                 if (denom < 1e-8) denom = 1e-8;
                 for (int r = 0; r < K; ++r)
-                    P->r_prob[r * JN + off] = dm_exp(-10.0 * (cum[r * JN + off] - mn) / denom);
+                    P->r_prob[r * JN + off] = P->cfg.ref_arith >= 3 ? exp(-10.0 * (cum[r * JN + off] - mn) / denom)
+                                                                    : dm_exp(-10.0 * (cum[r * JN + off] - mn) / denom);
                 double psum = blocked_sum(P->r_prob + off, JN, K, P->B);
                 for (int r = 0; r < K; ++r) P->r_prob[r * JN + off] /= psum;
                 /* computeParameterUpdates (policy_improvement.cpp:370-383) */
@@ -1571,6 +1608,13 @@ int so_get_last_trajectory(const so_problem* P, double* traj)
 {
     memcpy(traj, P->last_traj, sizeof(double) * (size_t)P->J * P->N);
     return 0;
+}
+
+int so_reuse_log(const so_problem* P, int* out, int cap)
+{
+    const int n = P->rank_n < cap ? P->rank_n : cap;
+    if (out && n > 0) memcpy(out, P->rank_log, sizeof(int) * (size_t)n);
+    return P->rank_n;
 }
 
 int so_get_rollouts(const so_problem* P, const char* which, double* out)

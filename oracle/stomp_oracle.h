@@ -128,7 +128,8 @@ typedef struct {
     const so_orientation_constraint* orientation_constraints;
     /* 1: the reference's written arithmetic order: non-fused dense L z / M eps and sequential
      * rollout sums over all K (instead of the engine's fma chain and 64-rollout blocks);
-     * 2: also VectorXd::sum() as Eigen 2's two-lane SSE2 packet reduction */
+     * 2: also VectorXd::sum() as Eigen 2's two-lane SSE2 packet reduction;
+     * 3: also the C library's exp / sin / cos / atan2 / asin where the reference calls them */
     int ref_arith;
 } so_config;
 
@@ -185,6 +186,9 @@ int so_get_last_trajectory(const so_problem* p, double* traj /* J x N */);
  * "state_costs" -> K x N; the extra rollout (addExtraRollouts): "x_params","x_noise",
  * "x_noise_projected","x_control_costs" -> J x N, "x_state_costs" -> N */
 int so_get_rollouts(const so_problem* p, const char* which, double* out);
+/* the reuse decisions so far: num_reused_rollouts candidate indices per ranking (-1 = the
+ * extra rollout), copied up to cap; returns how many there are */
+int so_reuse_log(const so_problem* p, int* out, int cap);
 
 /* stage primitives */
 void so_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

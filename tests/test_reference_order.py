@@ -8,7 +8,12 @@ arithmetic choices the reference does not:
   * sums over rollouts in fixed 64-rollout blocks, where the reference sums P and eps * P
     sequentially over all K (policy_improvement.cpp:352-358, 376-379).
 oracle ref_arith=1 follows the reference's written order instead (dense products, non-fused,
-one block).  Both modes share the same normals, so the difference is the arithmetic alone.
+one block); ref_arith=2 adds Eigen 2's packet VectorXd::sum(); ref_arith=3 adds the C library's
+exp (policy_improvement.cpp:356) and sin / cos (KDL Rot2 under
+treefksolverjointposaxis_partial.cpp:125) in place of the deterministic restatements the engine
+and the oracle share (oracle/dmath.h, csrc/stomp_math.h), which differ from glibc in the last
+bit on about a tenth of their inputs.  All modes share the same normals, so the difference is
+the arithmetic alone.
 North-star bar: best_group_trajectory_ within 1e-5 (BASELINE.json north_star); the observed
 drift is ~1e-14.  (Eigen 2's internal product blocking is third-party code that is not in
 the container, so its exact order stays unpinned)
@@ -30,7 +35,7 @@ def optimize_both(p, ref_mode):
     for ref in (0, ref_mode):
         o = po.Oracle(p, threads=THREADS, dense=bool(ref), ref_arith=ref)
         st, costs = o.optimize()
-        out.append((st, costs, o.best_trajectory(), o.last_trajectory(), o.theta()))
+        out.append((st, costs, o.best_trajectory(), o.last_trajectory(), o.theta(), o.reuse_log()))
     return out
 
 
@@ -42,20 +47,25 @@ CFG2 = dict(grid_n=256, num_rollouts=512, num_reused_rollouts=0, max_iterations=
 # 2: also Eigen 2's SSE2 packet reduction for VectorXd::sum() -- Rollout::getCost
 # (policy_improvement.cpp:149-156), which ranks the reused rollouts, and last_trajectory_cost_
 # (stomp_optimizer.cpp:1155), which picks the best iteration -- two interleaved lanes summed
-# at the end instead of index order (the decisions must hold under it too)
+# at the end instead of index order (the decisions must hold under it too);
+# 3: also glibc exp / sin / cos where the reference calls them (the libm boundary)
 @pytest.mark.parametrize("name,kw,ref_mode", [
     # cfg1 (BASELINE configs[0]): K=20, 10 reused, 128^3, 100 optimize iterations
-    ("cfg1", CFG1, 1), ("cfg1", CFG1, 2),
+    ("cfg1", CFG1, 1), ("cfg1", CFG1, 2), ("cfg1", CFG1, 3),
     # cfg2 (configs[1]): K=512, 256^3, 100 optimize iterations (parity after 1/10/100)
-    ("cfg2", CFG2, 1), ("cfg2", CFG2, 2),
+    ("cfg2", CFG2, 1), ("cfg2", CFG2, 2), ("cfg2", CFG2, 3),
 ])
 def test_engine_contract_vs_reference_order(name, kw, ref_mode):
     p = pb.make_problem(max_iterations_after_collision_free=1000, **kw)
-    (sa, ca, ba, la, ta), (sb, cb, bb, lb, tb) = optimize_both(p, ref_mode)
+    (sa, ca, ba, la, ta, ra), (sb, cb, bb, lb, tb, rb) = optimize_both(p, ref_mode)
     assert sa.iterations == sb.iterations == kw["max_iterations"]
     # the same decisions: collision-free streaks and best-iteration bookkeeping
     assert (sa.success, sa.success_iteration, sa.collision_success_iteration, sa.last_improvement_iteration) == \
         (sb.success, sb.success_iteration, sb.collision_success_iteration, sb.last_improvement_iteration)
+    # the same reuse decisions at every ranking (cfg1: 99 rankings of 21 candidates, 10 kept)
+    assert ra.shape == rb.shape == ((kw["max_iterations"] - 1, kw["num_reused_rollouts"])
+                                    if kw["num_reused_rollouts"] else (0, 1))
+    np.testing.assert_array_equal(ra, rb)
     d_best = np.abs(ba - bb).max()
     d_last = np.abs(la - lb).max()
     d_theta = np.abs(ta - tb).max()
@@ -78,3 +88,26 @@ def test_sequential_sums_equal_blocked_for_small_K():
         b.iterate(it)
     # identical normals and parameters up to the product rounding
     np.testing.assert_allclose(a.rollouts("noise"), b.rollouts("noise"), rtol=1e-12, atol=1e-13)
+
+
+def test_libm_boundary_is_exercised():
+    """ref_arith 3 is not vacuous: the shared deterministic exp / sin / cos differ from the C
+    library's in the last bit on a sizeable fraction of the arguments the path feeds them
+    (exp of -10 (S - min) / den in [-10, 0]; joint angles within a few radians), and the
+    mode-3 trajectory differs from mode 2's."""
+    import math
+    rng = np.random.default_rng(7)
+    xe = rng.uniform(-10.0, 0.0, 4000)
+    xs = rng.uniform(-3.2, 3.2, 4000)
+    de = sum(po.dexp(v) != math.exp(v) for v in xe)
+    ds = sum(po.dsincos(v)[0] != math.sin(v) or po.dsincos(v)[1] != math.cos(v) for v in xs)
+    # each within one ulp where they differ
+    assert max(abs(po.dexp(v) - math.exp(v)) / math.ulp(math.exp(v)) for v in xe) <= 1.0
+    assert de > 100 and ds > 100
+    p = pb.make_problem(grid_n=64, num_rollouts=10, num_reused_rollouts=5, max_iterations=10)
+    a = po.Oracle(p, dense=True, ref_arith=2)
+    b = po.Oracle(p, dense=True, ref_arith=3)
+    a.optimize()
+    b.optimize()
+    assert not np.array_equal(a.theta(), b.theta())
+    np.testing.assert_array_equal(a.reuse_log(), b.reuse_log())
