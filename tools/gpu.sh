@@ -20,6 +20,7 @@
 #   round R                  final R, then art R_cfgX for cfg1 / cfg3 / cfg4 / cfg5 and the
 #                            per-rank compute of the sharded shapes (gather 8 4 2, split 64 128 256)
 #   stamps LIB K [GRID DOF]  in-kernel phase stamps (tools/stamps.py) with the stamps library LIB
+#   micro                    FETCH_SIZE calibration of 2-byte scattered loads (tools/micro/gather_fetch)
 #   gather W ...             gather-mode ranks on one GPU (STOMP_DEBUG_GATHER_RANKS=W), cfg2
 #   split K ...              the sharded weights phases at per-rank K (STOMP_DEBUG_SHARDED_MODES)
 set -o pipefail
@@ -118,6 +119,15 @@ stamps)
   out=gpurun_out/stamps/$(basename $lib .so).$k.txt
   STOMP_ENGINE_LIB=$PWD/$lib timeout -k 10 120 python3 tools/stamps.py $k "$@" > $out 2>&1 || { tail -5 $out; exit 1; }
   head -40 $out ;;
+micro)
+  # FETCH_SIZE per line for 2-byte scattered loads (tools/micro/gather_fetch.hip, built on the CPU)
+  d=gpurun_out/micro; mkdir -p $d
+  i=0
+  for set in "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+    i=$((i+1))
+    timeout -k 10 120 rocprofv3 --pmc $set --output-format csv -d $d/p$i -o p$i -- tools/micro/gather_fetch $d/known.json > $d/p$i.log 2>&1 || { tail -20 $d/p$i.log; exit 1; }
+  done
+  python3 tools/micro/gather_fetch.py $d $d/gather_fetch.json ;;
 gather)
   mkdir -p gpurun_out/split
   for w in "$@"; do

@@ -4,7 +4,8 @@ summary bench.py reports as roofline.traffic.
 
 Counters (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are KiB per
 dispatch from the L2's memory-side request counters (Infinity-Cache hits included);
-on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled.  The
+on gfx950 FETCH_SIZE tallies every 128-B L2 line request at 64 B, so it is doubled (calibrated
+for the SDF gathers by tools/micro/gather_fetch.hip).  The
 rollout-cost stage is the fused k_rollout kernel (one launch per iteration).
 
 SQ_INSTS_VALU (VALU instructions issued, summed over the launch's waves) gives the VALU issue
@@ -77,11 +78,13 @@ def main():
         "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE TCC_HIT_sum TCC_MISS_sum | SQ_* (separate passes), "
                   "bench.py --workload " + workload + " --no-timing (tools/gpu.sh pmc); per-dispatch means",
         "workload": workload,
-        "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B, MI355X_MICROARCH.md:298, calibrated "
-                      "for wide coalesced reads); the SDF gathers are 4-B lane loads, for which the factor is "
-                      "uncalibrated, so the uncorrected figure (x1) is reported beside it: the true bytes lie "
-                      "between the two.  KiB -> B; Infinity-Cache hits are counted (memory side of L2), so this is "
-                      "L2-miss traffic, an upper bound on HBM bytes",
+        "correction": "FETCH_SIZE x2: gfx950 tallies every L2 miss (one 128-B line request) at 64 B, for wide "
+                      "coalesced reads (MI355X_MICROARCH.md:298) and for the SDF's 2-byte scattered gathers alike "
+                      "(tools/micro/gather_fetch.hip, profiles/r6_gather_fetch.txt: one 2-B load per distinct line "
+                      "and four per line both read 64.0 B per line touched, two or four far-apart loads per line "
+                      "128 / 256 B); the x1 figure is kept beside it for comparison with earlier rounds.  KiB -> B; "
+                      "Infinity-Cache hits are counted (memory side of L2), so this is L2-miss traffic, an upper "
+                      "bound on HBM bytes",
         "stage": stage[0] if stage else None,
         "source_hash": _build.embedded_hash(_build.LIB),   # the library the PMC passes ran
         "hbm_bytes_per_launch": sum(kernels[k].get("hbm_bytes", 0.0) for k in stage),
