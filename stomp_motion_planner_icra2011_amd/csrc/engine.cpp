@@ -543,7 +543,20 @@ void release(stomp_engine* e)
 // Task::execute of a launch's rollouts
 void launch_rollouts(stomp_engine* e, const CostArgs& ca)
 {
-    launch_cost(e->model, ca, e->stream);
+    DevModel& m = e->model;
+    const int nro = ca.num_noisy + (ca.x_params ? 1 : 0);
+    if (m.lean && m.nsaves > 0 && nro > m.sv_rows) {
+        // an eval batch with more rollouts than the lean layout's saved-frame blocks: grow them (the
+        // old blocks stay allocated until the engine is destroyed, launches before may use them)
+        double* nb = nullptr;
+        if (dev_alloc(e, &nb, (size_t)nro * m.nsaves * 12 * m.N) == 0) {
+            m.sv_glob = nb;
+            m.sv_rows = nro;
+        } else {
+            m.lean = 0;   // the full layout needs no saved-frame blocks
+        }
+    }
+    launch_cost(m, ca, e->stream);
 }
 
 // the state-cost terms after the collision cost (k_terms), on the rollouts a k_rollout
@@ -1620,6 +1633,31 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "rollout kernel needs %zu B of LDS (J=%d, N=%d, S=%d, %d spheres "
                                                     "on one segment), more than %zu", lds, J, N, e->S, m.sph_chunk,
                             kRolloutLdsMax));
+        // the LDS-lean slot-loop layout (DevModel::lean) when it puts more rollout workgroups on a
+        // CU and the launch has more workgroups than the full layout's slots: cfg3's N = 199 (71.7
+        // KB per workgroup, two per CU; lean 2 46.5 KB, three) and cfg4's two-arm tree (two saved
+        // frames, a 12 KB table)
+        m.lean = 0;
+        const int per_cu_full = rollout_blocks_per_cu(lds);
+        int per_cu[3] = {per_cu_full, 0, 0};
+        for (int lv = 1; lv <= 2; ++lv)
+            if (rollout_lean_allowed(m, lv)) per_cu[lv] = rollout_blocks_per_cu(rollout_lds_bytes(m, 0, lv) + stat, lv);
+        if (need > per_cu_full) {
+            int best = per_cu_full;
+            for (int lv = 1; lv <= 2; ++lv)
+                if (per_cu[lv] > best) {
+                    best = per_cu[lv];
+                    m.lean = lv;
+                }
+        }
+        if (const char* v = getenv("STOMP_DEBUG_LEAN")) {   // tests / A/B: force a layout
+            const int lv = atoi(v);
+            if (lv >= 0 && lv <= 2 && rollout_lean_allowed(m, lv)) m.lean = lv;
+        }
+        if (getenv("STOMP_DEBUG_LEAN_PRINT"))
+            fprintf(stderr, "stomp: rollout LDS full %zu / lean1 %zu / lean2 %zu B, workgroups per CU %d / %d / %d, "
+                            "needed %d, layout lean %d\n", lds, rollout_lds_bytes(m, 0, 1) + stat,
+                    rollout_lds_bytes(m, 0, 2) + stat, per_cu[0], per_cu[1], per_cu[2], need, m.lean);
     }
     if (!cost_supported(m)) CREATE_TRY(fail(e, STOMP_E_UNSUPPORTED, "FK program too large (%d ops, %d segments)",
                                             m.nops, m.nseg));
@@ -1702,6 +1740,10 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     // per rollout), and an eval batch may hold more rows than K_loc + 1
     m.split_cap = std::max(e->K_loc + 2, m.cus / 2 + 1);
     CREATE_TRY(dev_alloc(e, &m.split_cnt, (size_t)m.split_cap));
+    if (m.lean && m.nsaves > 0) {   // a [nsaves][12][N] block per rollout workgroup of a launch
+        m.sv_rows = e->K_loc + 1;
+        CREATE_TRY(dev_alloc(e, &m.sv_glob, (size_t)m.sv_rows * m.nsaves * 12 * N));
+    }
     {
         const char* env = std::getenv("STOMP_DEBUG_SPLIT_MAX");
         m.split_max = env ? std::atoi(env) : 0;

@@ -69,6 +69,62 @@ static_assert(kRunMaxSmall / 2 <= kLaneSpheres && kRunMaxLarge <= kLaneSpheres &
               "a pair lane's spheres of one run must fit kLaneSpheres");
 }
 
+// The lean layout's tables in HBM, typed in the constant address space: the kernel never writes
+// them, so a load through them with a wave-uniform index is a scalar load, which waits on the
+// scalar counter, not behind the vector memory counter of the gathers in flight.  The loaders copy
+// a record member by member into registers.
+using CSegment = const __attribute__((address_space(4))) DevSegment;
+using COp = const __attribute__((address_space(4))) FkOp;
+using CSphere = const __attribute__((address_space(4))) DevSphere;
+using CInt = const __attribute__((address_space(4))) int;
+using CDouble = const __attribute__((address_space(4))) double;
+__device__ __forceinline__ DevSegment load_seg(CSegment* p)
+{
+    DevSegment r;
+    r.parent = p->parent;
+    r.q_index = p->q_index;
+    r.rot_identity = p->rot_identity;
+    r.pad_ = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.rot[k] = p->rot[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        r.trans[k] = p->trans[k];
+        r.axis[k] = p->axis[k];
+    }
+    return r;
+}
+__device__ __forceinline__ FkOp load_op(COp* p)
+{
+    FkOp r;
+    r.seg = p->seg;
+    r.base = p->base;
+    r.save = p->save;
+    r.sph_begin = p->sph_begin;
+    r.sph_end = p->sph_end;
+    r.slot = p->slot;
+    return r;
+}
+__device__ __forceinline__ DevSphere load_sph(CSphere* p)
+{
+    DevSphere r;
+    r.slot = p->slot;
+    r.zero_lim = p->zero_lim;
+    r.col_lim = p->col_lim;
+    r.pad_ = 0;
+    r.radius = p->radius;
+    r.clearance = p->clearance;
+    r.inv_clearance = p->inv_clearance;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.pos[k] = p->pos[k];
+    return r;
+}
+// a pointer into HBM marked global (no flat instructions, which would wait on the LDS counter too)
+__device__ __forceinline__ double* global_ptr(double* p)
+{
+    return (double*)(__attribute__((address_space(1))) double*)p;
+}
+
 __device__ __forceinline__ void apply_lds(const double* fb, int N, int t, const double* pos, double* x)
 {
 #pragma unroll
@@ -165,9 +221,9 @@ __device__ __forceinline__ double sphere_speed(const DevModel& m, const double* 
 // together.  The argmax is a wave butterfly (every lane ends with the same (max, first
 // index)) and a pass needs no block barrier: LDS accesses of one wave execute in program order.
 // A joint without violations costs its wave one argmax.
-template <int NW>
-__device__ __forceinline__ void joint_limit_passes(const DevModel& m, double* traj, const int* hl_s,
-                                                   const double* jlim_s, int lane, int wv)
+template <int NW, typename IntTable, typename DoubleTable>
+__device__ __forceinline__ void joint_limit_passes(const DevModel& m, double* traj, IntTable hl_s,
+                                                   DoubleTable jlim_s, int lane, int wv)
 {
     const int J = m.J, N = m.N;
     // A wave keeps its joints' rows in registers through the passes (lane l: waypoints l,
@@ -296,14 +352,20 @@ __device__ __forceinline__ void spec_block(const CostArgs& a, int c, double* lds
 // slot's gathers are in flight (the running frame then stays live across the pair phases); off,
 // they advance after the fold from the frame reloaded from fb (fewer live registers: the grouped
 // launch, which is throughput-bound and register-capped at three workgroups per CU)
-template <int BLOCK, bool BRICK, bool PHASED = false, bool FK_OVERLAP = true>
+// LEAN (DevModel::lean, slot loop only): the saved branch-point frames in HBM (the workgroup's
+// block of sv_glob), no (sin, cos) pre-pass, the FK / joint-limit tables (and with LEAN 2 the sphere
+// table) read from the image in HBM through the constant address space, so their wave-uniform
+// loads are scalar loads that do not wait behind the vector memory counter of the gathers in flight
+template <int BLOCK, bool BRICK, bool PHASED = false, bool FK_OVERLAP = true, int LEAN = 0>
 __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& a, const int bid)
 {
+    static_assert(!LEAN || (!PHASED && FK_OVERLAP), "the lean layout is the slot loop's");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ int flag;
     __shared__ int nz_count;
     const int J = m.J, N = m.N, S = m.S;
-    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, m.pad_lds, PHASED);
+    const RolloutLds L = rollout_lds(J, N, S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, LEAN ? 0 : m.pad_lds,
+                                     PHASED, LEAN);
     {
         // blocks past the rollouts: the next iteration's pregen rows (normals, sigma L z,
         // M eps), left at the default wave priority while the rollout waves raise theirs, so
@@ -326,17 +388,31 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     if (a.stop && *a.stop) return;
     double* traj = (double*)(lds_raw + L.traj);   // J*N
     double* fb = (double*)(lds_raw + L.fb);       // 12*N frame of the current slot
-    double* sv = (double*)(lds_raw + L.sv);       // nsaves*12*N saved branch-point frames
+    // nsaves*12*N saved branch-point frames (LEAN: this workgroup's block of sv_glob in HBM)
+    double* sv = LEAN ? global_ptr(m.sv_glob) + (size_t)bid * m.nsaves * 12 * N : (double*)(lds_raw + L.sv);
     double* av = (double*)(lds_raw + L.av);       // max_slot*N: pot, then pot * |v|
     unsigned short* nzl = (unsigned short*)(lds_raw + L.nzl);   // pairs q*N+t with a non-zero potential
-    const DevSphere* sph = (const DevSphere*)(lds_raw + L.sph);
-    const DevSegment* seg_s = (const DevSegment*)(lds_raw + L.seg);
+    // the tables: LDS copies of the image, or (LEAN) the image in HBM (offsets relative to .sph)
+    const unsigned char* gimg = (const unsigned char*)m.img;
+    const DevSphere* sph = (const DevSphere*)(lds_raw + L.sph);   // not with LEAN 2
+    const DevSegment* seg_s = (const DevSegment*)(lds_raw + L.seg);   // not with LEAN
     const FkOp* ops_s = (const FkOp*)(lds_raw + L.ops);
-    const int* slot_sph_s = (const int*)(lds_raw + L.slot);
     const int* hl_s = (const int*)(lds_raw + L.hl);
     const double* jlim_s = (const double*)(lds_raw + L.jlim);
+    CSphere* csph = (CSphere*)gimg;
+    CSegment* cseg = (CSegment*)(gimg + (L.seg - L.sph));
+    COp* cops = (COp*)(gimg + (L.ops - L.sph));
+    CInt* chl = (CInt*)(gimg + (L.hl - L.sph));
+    CDouble* cjlim = (CDouble*)(gimg + (L.jlim - L.sph));
+    // the FK program's op i
+    auto op_at = [&](int i) -> FkOp {
+        if constexpr (LEAN != 0) return load_op(cops + i);
+        else return ops_s[i];
+    };
     // [12][S][3] padding-row sphere positions: LDS copy when it fits, else HBM
-    const double* pad = m.pad_lds ? (const double*)(lds_raw + L.pad) : m.pad_pos;
+    const double* pad = !LEAN && m.pad_lds ? (const double*)(lds_raw + L.pad) : m.pad_pos;
+    // every (sin, cos) made ahead of the FK program (the cosines in the saved-frame area)
+    const bool sincos_pre = !LEAN && m.sincos_pre;
 
     STAMP(0);
     BLOCK_BEGIN();
@@ -352,9 +428,12 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     const bool pre = a.fused_noise == 2 && !extra;
     constexpr int kCopyBatch = 12 * 256 / BLOCK;   // table-image words per lane per copy pass
     unsigned long long img[kCopyBatch];
-    const int nw = m.img_words;
+    // LEAN 1 copies the sphere table only, LEAN 2 nothing
+    const int nw = LEAN == 0 ? m.img_words : LEAN == 1 ? (int)(S * sizeof(DevSphere) / 8) : 0;
+    if constexpr (LEAN != 2) {
 #pragma unroll
-    for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
+        for (int u = 0; u < kCopyBatch; ++u) img[u] = m.img[min(tid + u * BLOCK, nw - 1)];
+    }
     // the pregen row's first chunk goes out with the image loads (one memory latency for both)
     PreChunk pc0;
     // a row priced by its pregen block (ctl_by_pre) needs no M eps here
@@ -390,7 +469,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         }
         if (xc) rollout_control<BLOCK>(a.nz, 0, zA, zB, tid, a.x_ctl);
     }
-    {
+    if constexpr (LEAN != 2) {
         unsigned long long* dst = (unsigned long long*)(lds_raw + L.sph);
 #pragma unroll
         for (int u = 0; u < kCopyBatch; ++u)
@@ -418,7 +497,8 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     // ---- handleJointLimits (no block-wide pre-scan: the barrier above already published traj)
     {
         __builtin_amdgcn_s_setprio(3);   // a dependent chain per joint (critical path)
-        joint_limit_passes<NW>(m, traj, hl_s, jlim_s, lane, wv);
+        if constexpr (LEAN != 0) joint_limit_passes<NW>(m, traj, chl, cjlim, lane, wv);
+        else joint_limit_passes<NW>(m, traj, hl_s, jlim_s, lane, wv);
         __builtin_amdgcn_s_setprio(2);
         __syncthreads();
     }
@@ -443,12 +523,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     double cum = 0.0, state = 0.0;
     bool col = false;
     // one FK program step (stomp_optimizer.cpp via treefksolverjointposaxis_partial.cpp:108-140)
-    auto fk_op = [&](const FkOp& o) {
-        if (o.seg < 0 || !fk_lane) return;
-        const DevSegment& sg = seg_s[o.seg];
+    auto fk_step = [&](const FkOp& o, const DevSegment& sg) {
         double st = 0.0, ct = 1.0;
         if (sg.q_index >= 0) {
-            if (m.sincos_pre) {
+            if (sincos_pre) {
                 st = traj[sg.q_index * N + t_own];
                 ct = sv[sg.q_index * N + t_own];
             } else {
@@ -478,17 +556,26 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
             for (int k = 0; k < 3; ++k) dst[(9 + k) * N] = C.p[k];
         }
     };
+    auto fk_op = [&](const FkOp& o) {
+        if (o.seg < 0 || !fk_lane) return;
+        if constexpr (LEAN != 0) {
+            const DevSegment sg = load_seg(cseg + o.seg);
+            fk_step(o, sg);
+        } else {
+            fk_step(o, seg_s[o.seg]);
+        }
+    };
     // run the program from op up to and including the next sphere-carrying segment; its
     // index (or nops) is uniform
     auto fk_advance = [&](int op) -> int {
         for (; op < m.nops; ++op) {
-            const FkOp o = ops_s[op];
+            const FkOp o = op_at(op);
             fk_op(o);
             if (o.sph_end > o.sph_begin) return op;   // a run of spheres on C
         }
         return m.nops;
     };
-    if (m.sincos_pre) {
+    if (sincos_pre) {
         // every joint angle's (sin, cos) by all lanes, three independent chains per lane, so the
         // FK lanes' chain is frame products only
         // (each element is read and overwritten by one lane; a clamped read past the end may see a
@@ -623,7 +710,7 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     int run = 0;   // sphere runs done (stamp index only)
     STAMP(7);
     while (op < m.nops) {
-        const FkOp o = ops_s[op];
+        const FkOp o = op_at(op);
         if (fk_lane) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) fb[k * N + t_own] = C.R[k];
@@ -656,7 +743,15 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform: no lane takes a u-th sphere of this run
-                const double* pos = sph[sb + min(pg + u * G, ns - 1)].pos;
+                double pos[3];
+                if constexpr (LEAN == 2) {   // G = 1: sphere u on every lane, a uniform index (scalar loads)
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) pos[i] = csph[sb + u].pos[i];
+                } else {
+                    const double* ps = sph[sb + min(pg + u * G, ns - 1)].pos;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) pos[i] = ps[i];
+                }
                 double x[3];
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
@@ -682,14 +777,21 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
 #pragma unroll
             for (int u = 0; u < kLaneSpheres; ++u) {
                 if (u * G >= ns) break;   // uniform
-                const int q = pg + u * G;
+                const int q = LEAN == 2 ? u : pg + u * G;   // LEAN 2: G = 1 and pg = 0 here
                 const bool in = q < ns;
                 bool nz = false;
                 if (in) {
-                    const DevSphere& sp = sph[sb + q];
+                    int zl, cl;
+                    if constexpr (LEAN == 2) {
+                        zl = csph[sb + q].zero_lim;
+                        cl = csph[sb + q].col_lim;
+                    } else {
+                        zl = sph[sb + q].zero_lim;
+                        cl = sph[sb + q].col_lim;
+                    }
                     const int d2 = (okm >> u) & 1u ? (int)dv[u] : 0;
-                    col |= d2 < sp.col_lim;
-                    nz = d2 < sp.zero_lim;
+                    col |= d2 < cl;
+                    nz = d2 < zl;
                     // a non-zero pair keeps its d2 until the velocity phase prices it; a = pot * |v|
                     // is +0 exactly when pot == +0
                     av[q * N + pt] = nz ? (double)d2 : 0.0;
@@ -713,9 +815,15 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
         for (int i = tid; i < nz_count; i += BLOCK) {
             const int it = nzl[i];
             const int qi = it / N, ti = it - qi * N;
-            const DevSphere& sp = sph[sb + qi];
-            const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
-            av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
+            if constexpr (LEAN == 2) {
+                const DevSphere sp = load_sph(csph + sb + qi);
+                const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
+                av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
+            } else {
+                const DevSphere& sp = sph[sb + qi];
+                const double pot = potential(sp, sdf_metres(m, (unsigned)av[it]));
+                av[it] = pot * sphere_speed(m, fb, pad, sp, sb + qi, ti);
+            }
         }
         if constexpr (!FK_OVERLAP) {
             // C is reloaded from fb (not kept live across the pairs)
@@ -777,10 +885,10 @@ __device__ __forceinline__ void rollout_body(const DevModel& m, const CostArgs& 
     BLOCK_END();
 }
 
-template <int BLOCK, bool BRICK>
+template <int BLOCK, bool BRICK, int LEAN = 0>
 __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout(DevModel m, CostArgs a)
 {
-    rollout_body<BLOCK, BRICK>(m, a, blockIdx.x);
+    rollout_body<BLOCK, BRICK, false, true, LEAN>(m, a, blockIdx.x);
 }
 
 // the phased evaluation for launches whose rollouts run one per CU (LDS: rollout_lds phased)
@@ -1320,9 +1428,10 @@ bool cost_supported(const DevModel& m)
     return m.nops <= kMaxOps && m.nseg <= kMaxSeg && m.nslots <= kMaxSeg && m.J <= kMaxJoints && m.N <= kBlock;
 }
 
-size_t rollout_lds_bytes(const DevModel& m, int pad_lds)
+size_t rollout_lds_bytes(const DevModel& m, int pad_lds, int lean)
 {
-    return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, pad_lds).total;
+    return rollout_lds(m.J, m.N, m.S, m.sph_chunk, m.nsaves, m.nseg, m.nops, m.nslots, lean ? 0 : pad_lds, false,
+                       lean).total;
 }
 
 size_t rollout_phased_lds_bytes(const DevModel& m)
@@ -1345,11 +1454,18 @@ size_t rollout_static_lds()
 // resident rollout workgroups per CU for a given total LDS per workgroup: the smaller of
 // the LDS limit and the register limit (4 SIMDs, 512 VGPRs per lane-slot, 8-register
 // granules; MI355X_MICROARCH.md occupancy table)
-int rollout_blocks_per_cu(size_t lds_total)
+bool rollout_lean_allowed(const DevModel& m, int lean)
+{
+    return lean == 0 || lean == 1 || (lean == 2 && m.N > kBlock / 2 && m.N <= kBlock);
+}
+
+int rollout_blocks_per_cu(size_t lds_total, int lean)
 {
     hipFuncAttributes attr;
     int regs = 256;
-    if (hipFuncGetAttributes(&attr, (const void*)k_rollout<kBlock, false>) == hipSuccess && attr.numRegs > 0)
+    const void* fn = lean == 2 ? (const void*)k_rollout<kBlock, false, 2>
+                   : lean == 1 ? (const void*)k_rollout<kBlock, false, 1> : (const void*)k_rollout<kBlock, false>;
+    if (hipFuncGetAttributes(&attr, fn) == hipSuccess && attr.numRegs > 0)
         regs = attr.numRegs;
     const int alloc = (regs + 7) / 8 * 8;
     int waves_per_simd = 512 / alloc;
@@ -1388,6 +1504,19 @@ static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
     if (kWideBlock != kBlock && nro <= m.cus) {
         if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kWideBlock, BRICK>, lds);
         hipLaunchKernelGGL((k_rollout<kWideBlock, BRICK>), dim3(blocks), dim3(kWideBlock), lds, s, m, a);
+        return;
+    }
+    if (m.lean) {
+        // the LDS-lean layout (DevModel::lean): sv_glob holds a block per rollout workgroup
+        assert(nro <= m.sv_rows || m.nsaves == 0);
+        const size_t ll = rollout_lds_bytes(m, 0, m.lean);
+        if (m.lean == 2) {
+            if (ll > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK, 2>, ll);
+            hipLaunchKernelGGL((k_rollout<kBlock, BRICK, 2>), dim3(blocks), dim3(kBlock), ll, s, m, a);
+        } else {
+            if (ll > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK, 1>, ll);
+            hipLaunchKernelGGL((k_rollout<kBlock, BRICK, 1>), dim3(blocks), dim3(kBlock), ll, s, m, a);
+        }
         return;
     }
     if (lds > 64 * 1024) lds_opt_in((const void*)k_rollout<kBlock, BRICK>, lds);

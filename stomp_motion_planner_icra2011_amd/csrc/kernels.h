@@ -102,6 +102,16 @@ struct DevModel {
                                 // eval batches included); split_pieces refuses larger launches
     int split_cap;
     int split_max;              // most pieces per rollout (STOMP_DEBUG_SPLIT_MAX, read at creation)
+    // LDS-lean slot-loop layout (rollout_lds lean > 0), chosen at creation when it fits more rollout
+    // workgroups on a CU than the full layout and the launch has more workgroups than the full
+    // layout's slots (cfg3's N = 199, cfg4's two-arm tree): 1 = the saved branch-point frames in HBM
+    // (sv_glob, one [nsaves][12][N] block per rollout workgroup of a launch), no (sin, cos) pre-pass
+    // (its cosines parked in the saved-frame area), and the FK / joint-limit tables read from the
+    // image in HBM through the scalar cache; 2 = also the sphere table (only with one pair-lane
+    // group, N > kBlock / 2, where a run's sphere index is uniform)
+    int lean;
+    double* sv_glob;
+    int sv_rows;                // rollout workgroups sv_glob holds (>= every lean launch's nro)
 };
 
 
@@ -121,14 +131,14 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t
 __host__ __device__ inline int noise_jp(int J) { return (J + kNoiseJT - 1) / kNoiseJT * kNoiseJT; }
 
 __host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_slot, int nsaves, int nseg, int nops,
-                                                  int nslots, int pad_lds, bool phased = false)
+                                                  int nslots, int pad_lds, bool phased = false, int lean = 0)
 {
     RolloutLds l;
     if (phased) max_slot = S;
     l.traj = 0;
     l.fb = l.traj + (size_t)J * N * sizeof(double);
     l.sv = l.fb + (size_t)(phased ? nslots : 1) * 12 * N * sizeof(double);
-    l.av = l.sv + (size_t)nsaves * 12 * N * sizeof(double);
+    l.av = l.sv + (size_t)(lean ? 0 : nsaves) * 12 * N * sizeof(double);
     l.nzl = l.av + (size_t)max_slot * N * sizeof(double);
     // noise phase: A = z then x (padded), B = eps then the control-cost terms
     const size_t nzw = (size_t)(N + kBandBatch) * noise_jp(J) > (size_t)J * (N + 12)
@@ -148,6 +158,9 @@ __host__ __device__ inline RolloutLds rollout_lds(int J, int N, int S, int max_s
     l.jlim = align16(l.hl + (size_t)J * sizeof(int));
     l.pad = align16(l.jlim + (size_t)2 * J * sizeof(double));
     l.total = l.pad + (pad_lds ? (size_t)36 * S * sizeof(double) : 0);
+    if (lean) {   // only the sphere table (lean 1) stays in LDS; no padding positions
+        l.total = lean == 1 ? l.seg : l.sph;
+    }
     return l;
 }
 
@@ -367,10 +380,11 @@ void launch_track(DevTrack* tr, int it, int max_it_cf, const double* total, cons
                   double* costs, const double* last_traj, double* best_traj, int JN, hipStream_t s);
 void launch_cost(const DevModel& m, const CostArgs& a, hipStream_t s);
 bool cost_supported(const DevModel& m);
-size_t rollout_lds_bytes(const DevModel& m, int pad_lds);   // dynamic LDS of the rollout kernel
+size_t rollout_lds_bytes(const DevModel& m, int pad_lds, int lean = 0);   // dynamic LDS of the rollout kernel
 size_t rollout_phased_lds_bytes(const DevModel& m);        // of the phased wide rollout, 0: does not fit
 size_t rollout_static_lds();                                 // its static LDS
-int rollout_blocks_per_cu(size_t lds_total);                 // occupancy (LDS and register limits)
+int rollout_blocks_per_cu(size_t lds_total, int lean = 0);   // occupancy (LDS and register limits)
+bool rollout_lean_allowed(const DevModel& m, int lean);       // lean 2 needs one pair-lane group
 // LDS per CU is 160 KiB (MI355X_MICROARCH.md), but three 49.5 KB rollout workgroups did not
 // co-reside on one CU in our residency measurements (tools/stamps.py) while three 46.9 KB
 // ones did, so the occupancy model budgets 144 KiB

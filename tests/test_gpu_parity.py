@@ -122,6 +122,29 @@ def test_brick_layout_bitwise(monkeypatch, grid_n, K):
         assert bool(cf[r]) == ocf
 
 
+@pytest.mark.parametrize("dof,waypoints,lean", [(7, 200, 2), (7, 200, 1), (14, 100, 1), (7, 100, 1)])
+def test_lean_layout_bitwise(monkeypatch, capfd, dof, waypoints, lean):
+    # the LDS-lean slot-loop layout (DevModel::lean: saved branch-point frames in HBM, the FK and
+    # joint-limit tables through the scalar cache, no (sin, cos) pre-pass; lean 2 also the sphere
+    # table), forced at K = 300 (more rollouts than CUs, so the launch takes the slot loop):
+    # bit-identical to the oracle, and an eval batch larger than the saved-frame blocks made at
+    # creation grows them
+    monkeypatch.setenv("STOMP_DEBUG_LEAN", str(lean))
+    monkeypatch.setenv("STOMP_DEBUG_LEAN_PRINT", "1")
+    p = make(dof=dof, waypoints=waypoints, K=300)
+    o, e = po.Oracle(p, threads=8), eng.Engine(p)
+    assert f"layout lean {lean}" in capfd.readouterr().err
+    for it in range(1, 4):
+        _compare_iteration(o, e, it)
+    rng = np.random.default_rng(9)
+    params = o.theta()[None] + rng.standard_normal((320, p.J, p.N)).cumsum(axis=2) * 0.05
+    costs, cf, _ = e.execute(params, iteration_member=1)
+    for r in range(0, 320, 37):
+        oc, ocf, _ = o.execute(params[r], iteration_member=1)
+        np.testing.assert_array_equal(costs[r], oc)
+        assert bool(cf[r]) == ocf
+
+
 def test_refresh_field_after_an_in_place_rebuild(monkeypatch):
     # a device field the engine copies into its bricked layout (the default past 64 MiB; forced
     # here at 64^3): after the caller rebuilds its buffer in place, stomp_engine_refresh_field

@@ -2,7 +2,7 @@
 
 Needs the stamps library (python -m stomp_motion_planner_icra2011_amd._build --stamps); never
 used for timing claims (the stamps serialise the kernels they instrument).
-Usage: STOMP_ENGINE_LIB=.../libstomp_engine_stamps.so python tools/stamps.py [K] [grid] [dof] [K_r]
+Usage: STOMP_ENGINE_LIB=.../libstomp_engine_stamps.so python tools/stamps.py [K] [grid] [dof] [K_r] [waypoints]
 """
 import ctypes as C
 import os
@@ -18,8 +18,9 @@ K = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 G = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 DOF = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 KR = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+WP = int(sys.argv[5]) if len(sys.argv) > 5 else 100
 lib = eng.load_library()
-p = pb.make_problem(dof=DOF, grid_n=G, num_rollouts=K, num_reused_rollouts=KR, build_grid=False)
+p = pb.make_problem(dof=DOF, waypoints=WP, grid_n=G, num_rollouts=K, num_reused_rollouts=KR, build_grid=False)
 sdf = eng.DeviceBuffer(4 * G ** 3)
 eng.sdf_build_device(p, sdf.ptr)
 e = eng.Engine(p, sdf_device_ptr=sdf.ptr)
