@@ -916,7 +916,11 @@ __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_g
         p = j / npre;
         bid = nro + (j - p * npre);
     }
-    rollout_body<BLOCK, BRICK, false, false>(ms[p], as[p], bid);
+    // the per-engine models and arguments read through the constant address space: wave-uniform
+    // scalar loads the compiler may repeat, as it does for a kernel argument
+    using CModel = const __attribute__((address_space(4))) DevModel;
+    using CArgs = const __attribute__((address_space(4))) CostArgs;
+    rollout_body<BLOCK, BRICK, false, false>(*(const DevModel*)((CModel*)ms + p), *(const CostArgs*)((CArgs*)as + p), bid);
 }
 
 // ---- the waypoint-split rollout (k_rollout_split): when a launch's rollouts fit P >= 2 to a CU

@@ -435,7 +435,9 @@ __global__ __launch_bounds__(BLOCK) void k_weights_rows_group(const WeightArgs* 
 {
     extern __shared__ __attribute__((aligned(16))) double V[];
     const int p = blockIdx.x / nt;
-    weights_rows<BLOCK, TCW, EPT>(as[p], blockIdx.x - p * nt, nt, V);
+    // the engine's arguments through the constant address space (scalar loads, as a kernel argument)
+    using CArgs = const __attribute__((address_space(4))) WeightArgs;
+    weights_rows<BLOCK, TCW, EPT>(*(const WeightArgs*)((CArgs*)as + p), blockIdx.x - p * nt, nt, V);
 }
 
 // K_loc <= 64 (one canonical block), FUSED: one wave per flat column c = d N + t, lane r = rollout
@@ -654,7 +656,8 @@ __global__ __launch_bounds__(256) void k_update(int J, int N, const double* MT, 
 __global__ __launch_bounds__(256) void k_update_group(int J, int N, const UpdateArgs* as)
 {
     const int p = blockIdx.x / J;
-    const UpdateArgs& a = as[p];
+    using CArgs = const __attribute__((address_space(4))) UpdateArgs;   // scalar loads, as a kernel argument
+    const UpdateArgs& a = *(const UpdateArgs*)((CArgs*)as + p);
     update_body(blockIdx.x - p * J, J, N, a.MT, a.u, nullptr, 0, a.theta, a.stop, nullptr);
 }
 
