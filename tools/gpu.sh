@@ -15,7 +15,8 @@
 #   pmc TAG [ARGS]           the PMC passes (FETCH_SIZE; WRITE_SIZE + TCC hit/miss; SQ counters),
 #                            each its own rocprofv3 run, over bench.py ARGS -> gpurun_out/TAG/
 #   art R [ARGS]             round artifacts of one workload: prof + pmc + tools/pmc_traffic.py
-#                            summary (gpurun_out/art_R/traffic.json) + its bench line
+#                            summary (gpurun_out/art_R/traffic.json) + its bench line (with that
+#                            summary and the CPU baselines, ART_CPU seconds, default 12)
 #   final R                  tests + smoke + art R for cfg2 + the driver-shape bench line
 #   round R                  final R, then art R_cfgX for cfg1 / cfg3 / cfg4 / cfg5 and the
 #                            per-rank compute of the sharded shapes (gather 8 4 2, split 64 128 256)
@@ -95,7 +96,10 @@ art)
   wl=cfg2; prev=""
   for a in "$@"; do [ "$prev" = "--workload" ] && wl=$a; prev=$a; done
   python3 tools/pmc_traffic.py gpurun_out/art_${r}_pmc gpurun_out/art_$r/traffic.json gpurun_out/art_$r/kernel_stats.csv $wl || exit 1
-  bench_to gpurun_out/art_$r/bench.json 500 --cpu-seconds 0 "$@" || exit 1
+  # the bench line reads the PMC summary of its own build from profiles/ (bench.py pmc_summary):
+  # this box's copy, so the line carries traffic and VALU (commit traffic.json under profiles/)
+  cp gpurun_out/art_$r/traffic.json profiles/_box_${r}_rollout_cost_traffic.json
+  bench_to gpurun_out/art_$r/bench.json 500 --cpu-seconds ${ART_CPU:-12} "$@" || exit 1
   cat gpurun_out/art_$r/bench.json ;;
 final)
   r=$1
