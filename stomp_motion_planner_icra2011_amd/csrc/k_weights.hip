@@ -247,8 +247,9 @@ template <int BLOCK, int TCW, int EPT>
 __device__ __forceinline__ void weights_rows(const WeightArgs& a, int bid, int nt, double* V)
 {
     constexpr int RS = BLOCK / TCW;
-    __shared__ double red0[BLOCK], red1[BLOCK];
-    __shared__ double part[BLOCK];
+    // the per-wave extremes of the tile's columns, and the block partials (nb TCW <= 256, rows_tcw)
+    __shared__ double red0[BLOCK / 64 * TCW], red1[BLOCK / 64 * TCW];
+    __shared__ double part[256];
     __shared__ double ps_s[TCW];
     if (a.stop && *a.stop) return;
     const int N = a.N, J = a.J, K = a.K_loc;
@@ -557,6 +558,8 @@ void launch_weights(const WeightArgs& a, hipStream_t s)
         if (K <= 16 * 64) return launch_rows_t<256, 4, 16>(a, s);
         return launch_rows_t<256, 4, 32>(a, s);
     case 2:
+        // (512 lanes with 16 rows each: 159 VGPRs, one workgroup per CU, 96.5 against 81 us at
+        // cfg3, profiles/ab/r6_weights_512.txt)
         return launch_rows_t<256, 2, 32>(a, s);
     default:
         break;
