@@ -425,6 +425,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # STOMP_BENCH_DEVICE: every rank on this device (a multi-rank rehearsal on a one-GPU box)
+    local_rank = int(os.environ.get("STOMP_BENCH_DEVICE", local_rank))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     if args.workload == "cfg5":
