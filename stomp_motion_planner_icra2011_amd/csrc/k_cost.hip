@@ -350,8 +350,8 @@ __device__ __forceinline__ void spec_block(const CostArgs& a, int c, double* lds
 // k_rollout_group: the engines of a group share one launch)
 // FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
 // slot's gathers are in flight (the running frame then stays live across the pair phases); off,
-// they advance after the fold from the frame reloaded from fb (fewer live registers: the grouped
-// launch, which is throughput-bound and register-capped at three workgroups per CU)
+// they advance after the fold from the frame reloaded from fb (fewer live registers; every launch
+// now overlaps)
 // LEAN (DevModel::lean, slot loop only): the saved branch-point frames in HBM (the workgroup's
 // block of sv_glob), no (sin, cos) pre-pass, the FK / joint-limit tables (and with LEAN 2 the sphere
 // table) read from the image in HBM through the constant address space, so their wave-uniform
@@ -920,7 +920,10 @@ __global__ __launch_bounds__(BLOCK, rollout_min_waves<BLOCK>()) void k_rollout_g
     // scalar loads the compiler may repeat, as it does for a kernel argument
     using CModel = const __attribute__((address_space(4))) DevModel;
     using CArgs = const __attribute__((address_space(4))) CostArgs;
-    rollout_body<BLOCK, BRICK, false, false>(*(const DevModel*)((CModel*)ms + p), *(const CostArgs*)((CArgs*)as + p), bid);
+    // the FK advance overlaps the gathers here too: with the arguments in the constant address space
+    // the grouped kernel fits it in 162 VGPRs without spilling (it had spilled 104 B per lane with
+    // the generic-pointer arguments, round 3)
+    rollout_body<BLOCK, BRICK, false, true>(*(const DevModel*)((CModel*)ms + p), *(const CostArgs*)((CArgs*)as + p), bid);
 }
 
 // ---- the waypoint-split rollout (k_rollout_split): when a launch's rollouts fit P >= 2 to a CU

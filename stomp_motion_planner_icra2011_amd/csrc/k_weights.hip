@@ -670,29 +670,40 @@ void launch_update_group(int J, int N, const UpdateArgs* as, int engines, hipStr
 }
 
 // the rows path of launch_weights for a group (the engine checks weights_group_tiles() > 0)
+// columns per tile of the grouped weights launch: eight while K_loc <= 128 (a group's launch has
+// engines x tiles workgroups, many rounds of them: wider tiles halve the rounds at the same per-lane
+// work, since a tile's time is its dependent phases, not its columns; cfg5 65 -> 44 us,
+// profiles/ab/r6_group_weights_fk.txt), else four
+static int group_tcw(int K_loc)
+{
+    return K_loc <= 128 && (K_loc + kSumBlock - 1) / kSumBlock * 8 <= 256 ? 8 : 4;
+}
+
 int weights_group_tiles(int J, int N, int K_loc)
 {
     if (rows_tcw(K_loc) != 4) return 0;
-    return (J * N + 3) / 4;
+    const int tcw = group_tcw(K_loc);
+    return (J * N + tcw - 1) / tcw;
 }
 
-template <int BLOCK, int EPT>
+template <int BLOCK, int TCW, int EPT>
 static void launch_rows_group_t(const WeightArgs* as, int engines, int nt, int K_loc, hipStream_t s)
 {
-    const size_t lds = weights_rows_v_bytes(K_loc, 4);
-    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<BLOCK, 4, EPT>, lds);
-    hipLaunchKernelGGL((k_weights_rows_group<BLOCK, 4, EPT>), dim3(nt * engines), dim3(BLOCK), lds, s, as, nt);
+    const size_t lds = weights_rows_v_bytes(K_loc, TCW);
+    if (lds > 48 * 1024) lds_opt_in((const void*)k_weights_rows_group<BLOCK, TCW, EPT>, lds);
+    hipLaunchKernelGGL((k_weights_rows_group<BLOCK, TCW, EPT>), dim3(nt * engines), dim3(BLOCK), lds, s, as, nt);
 }
 
 void launch_weights_group(const WeightArgs* as, int engines, int J, int N, int K_loc, hipStream_t s)
 {
     const int nt = weights_group_tiles(J, N, K_loc);
     if (nt <= 0 || engines <= 0) return;
-    if (K_loc <= 4 * 64) return launch_rows_group_t<256, 4>(as, engines, nt, K_loc, s);
-    if (K_loc <= 4 * 128) return launch_rows_group_t<512, 4>(as, engines, nt, K_loc, s);
-    if (K_loc <= 8 * 128) return launch_rows_group_t<512, 8>(as, engines, nt, K_loc, s);
-    if (K_loc <= 16 * 64) return launch_rows_group_t<256, 16>(as, engines, nt, K_loc, s);
-    return launch_rows_group_t<256, 32>(as, engines, nt, K_loc, s);
+    if (group_tcw(K_loc) == 8) return launch_rows_group_t<256, 8, 4>(as, engines, nt, K_loc, s);   // 32 rows a pass
+    if (K_loc <= 4 * 64) return launch_rows_group_t<256, 4, 4>(as, engines, nt, K_loc, s);
+    if (K_loc <= 4 * 128) return launch_rows_group_t<512, 4, 4>(as, engines, nt, K_loc, s);
+    if (K_loc <= 8 * 128) return launch_rows_group_t<512, 4, 8>(as, engines, nt, K_loc, s);
+    if (K_loc <= 16 * 64) return launch_rows_group_t<256, 4, 16>(as, engines, nt, K_loc, s);
+    return launch_rows_group_t<256, 4, 32>(as, engines, nt, K_loc, s);
 }
 
 void launch_update(int J, int N, const double* MT, const double* u, const double* u_all, int nb_total, double* theta,
