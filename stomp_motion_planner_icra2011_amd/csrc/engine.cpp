@@ -547,13 +547,16 @@ void launch_rollouts(stomp_engine* e, const CostArgs& ca)
     const int nro = ca.num_noisy + (ca.x_params ? 1 : 0);
     if (m.lean && m.nsaves > 0 && nro > m.sv_rows) {
         // an eval batch with more rollouts than the lean layout's saved-frame blocks: grow them (the
-        // old blocks stay allocated until the engine is destroyed, launches before may use them)
-        double* nb = nullptr;
-        if (dev_alloc(e, &nb, (size_t)nro * m.nsaves * 12 * m.N) == 0) {
-            m.sv_glob = nb;
+        // old blocks stay allocated until the engine is destroyed, launches before may use them).
+        // Without the memory the engine takes the full layout, which is valid for every launch.
+        void* q = nullptr;
+        if (hipMalloc(&q, sizeof(double) * (size_t)nro * m.nsaves * 12 * m.N) == hipSuccess) {
+            e->allocs.push_back(q);
+            m.sv_glob = (double*)q;
             m.sv_rows = nro;
         } else {
-            m.lean = 0;   // the full layout needs no saved-frame blocks
+            (void)hipGetLastError();
+            m.lean = 0;
         }
     }
     launch_cost(m, ca, e->stream);
