@@ -151,6 +151,8 @@ struct stomp_engine {
     // [K + 1][J][N] each (row K the extra rollout); spec_on: allocated (STOMP_DEBUG_NO_SPEC=1: not)
     double *d_spec_params = nullptr, *d_spec_noise = nullptr, *d_spec_ctl = nullptr;
     bool spec_on = false;
+    // the copy of the chosen candidates in the weights launch (STOMP_DEBUG_NO_PICK_FUSE=1: k_reuse_pick)
+    bool pick_fuse = true;
     int* d_sel = nullptr;
     uint8_t* d_cf = nullptr;
     uint16_t* d_sdf = nullptr;   // d2 per voxel (the engine's bricked copy when model.brick)
@@ -952,6 +954,9 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
     }
     if (e->gather)
         if (int rc = exchange_state(e)) return rc;
+    // the reuse step folded into the one-wave-per-column weights (launch_weights_pick)
+    ReuseArgs pick_ra{};
+    bool pick_in_weights = false;
     if (reuse_late) {
         // the previous rows and the extra rollout (evaluated just now) ranked; the reused rows'
         // projection and control costs after them.  On one device the candidates' totals are
@@ -967,7 +972,13 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
             Timed tm(e, T_NOISE);
             if (spec) {
                 ra.spec_params = e->d_spec_params; ra.spec_noise = e->d_spec_noise; ra.spec_ctl = e->d_spec_ctl;
-                launch_reuse_pick(na, ra, e->stream);
+                // (launch_weights_pick_ok decides at the weights launch; otherwise k_reuse_pick runs there)
+                if (e->pick_fuse && !e->split_modes && !e->use_cum) {
+                    pick_ra = ra;
+                    pick_in_weights = true;
+                } else {
+                    launch_reuse_pick(na, ra, e->stream);
+                }
             } else {
                 launch_reuse_rows(na, ra, e->stream);
             }
@@ -992,7 +1003,12 @@ int enqueue_iteration(stomp_engine* e, int it, bool pipelined)
         if (e->use_cum) launch_cumulative(wa, e->d_cum, e->stream);
         if (!e->split_modes) {
             wa.mode = W_FUSED;
-            launch_weights(wa, e->stream);
+            if (pick_in_weights && launch_weights_pick_ok(wa, pick_ra)) {
+                launch_weights_pick(wa, pick_ra, na.params, na.noise, na.control, e->stream);
+            } else {
+                if (pick_in_weights) launch_reuse_pick(na, pick_ra, e->stream);
+                launch_weights(wa, e->stream);
+            }
         } else {
             // the sharded decomposition; with one rank (debug hook) the all-reduce is the
             // identity and the all-gathers are device copies
@@ -1492,6 +1508,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
             CREATE_TRY(dev_alloc(e, &e->d_spec_ctl, n));
             e->spec_on = true;
         }
+        const char* no_fuse = std::getenv("STOMP_DEBUG_NO_PICK_FUSE");
+        e->pick_fuse = !(no_fuse && std::strcmp(no_fuse, "1") == 0);
     }
     if (e->world > 1 && e->Kr > 0) {
         const size_t slot = (size_t)e->Kr * ((size_t)J * N + N);

@@ -453,26 +453,21 @@ __device__ __forceinline__ double readlane_f64(double x, int l)
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
-__global__ __launch_bounds__(256) void k_weights_wave(WeightArgs a)
+// the column of a wave of the XCD-grouped four-column tiles
+__device__ __forceinline__ int wave_column()
 {
-    if (a.stop && *a.stop) return;
-    const int N = a.N, JN = a.J * N, K = a.K_loc;
     const int nt = gridDim.x, bid = blockIdx.x;
     const int x = bid & 7, q8 = nt >> 3, r8 = nt & 7;
     const int tile = x * q8 + min(x, r8) + (bid >> 3);
-    const int c = __builtin_amdgcn_readfirstlane(tile * 4 + (int)(threadIdx.x >> 6));
-    if (c >= JN) return;   // the whole wave
-    const int lane = threadIdx.x & 63, t = c % N;
+    return __builtin_amdgcn_readfirstlane(tile * 4 + (int)(threadIdx.x >> 6));
+}
+
+// column c's probabilities and update term from lane r's cost v and noise nz (r < K live)
+__device__ __forceinline__ void wave_weights(const WeightArgs& a, int c, int lane, int K, double v, double nz)
+{
+    const int JN = a.J * a.N;
     const bool live = lane < K;
     const size_t r = (size_t)min(lane, K - 1);
-    const double nz = a.noise[r * JN + c];
-    double v;
-    if (a.cum) {
-        v = a.cum[r * JN + c];
-    } else {
-        const double st = a.state[r * N + t], ct = a.control[r * JN + c];
-        v = st + ct;
-    }
     double mn = live ? v : __builtin_inf(), mx = live ? v : -__builtin_inf();
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -508,7 +503,173 @@ __global__ __launch_bounds__(256) void k_weights_wave(WeightArgs a)
     if (lane == 0) a.u[c] = 0.0 + s2;
 }
 
+__global__ __launch_bounds__(256) void k_weights_wave(WeightArgs a)
+{
+    if (a.stop && *a.stop) return;
+    const int N = a.N, JN = a.J * N, K = a.K_loc;
+    const int c = wave_column();
+    if (c >= JN) return;   // the whole wave
+    const int lane = threadIdx.x & 63, t = c % N;
+    const size_t r = (size_t)min(lane, K - 1);
+    const double nz = a.noise[r * JN + c];
+    double v;
+    if (a.cum) {
+        v = a.cum[r * JN + c];
+    } else {
+        const double st = a.state[r * N + t], ct = a.control[r * JN + c];
+        v = st + ct;
+    }
+    wave_weights(a, c, lane, K, v, nz);
+}
+
+// k_weights_wave with k_reuse_pick folded in (one device, every candidate priced by the rollout
+// launch, K < 64, no cumulative costs): lane l <= K holds candidate l's priced values at the
+// wave's column (row K the extra rollout) beside its own generated row's (l < K_gen), all loaded
+// in one round trip; every wave ranks the K previous totals itself (lane l's (total, index)
+// rank, reuse_choice's order) and each workgroup makes the extra rollout's total from its cost
+// rows staged in LDS (candidate_total's t-chains, one lane per row); reused row rr = l - K_gen
+// takes the candidate reuse_choice chooses for rank rr by a lane shuffle, writes its params,
+// noise and control at the column (and state, column t of joint 0) and prices it with the rest:
+// the rows k_reuse_pick copies, with no launch between the rollouts and the weights.  LDS:
+// (J + 1) N doubles when the extra rollout is a candidate.
+constexpr int kPickStageLoads = 8;   // the extra rollout's (J + 1) N <= 2048 cost values, one pass
+
+__global__ __launch_bounds__(256) void k_weights_wave_pick(WeightArgs a, ReuseArgs ra, double* params, double* noise,
+                                                           double* control)
+{
+    extern __shared__ __attribute__((aligned(16))) double stage[];   // [J + 1][N]
+    if (a.stop && *a.stop) return;
+    STAMP(10);
+    const int N = a.N, J = a.J, JN = J * N, K = a.K_loc, Kp = ra.K, Kg = ra.K_gen, P = (J + 1) * N;
+    const int c = wave_column();
+    const bool cok = c < JN;   // wave-uniform; a wave past the columns still joins the barrier
+    const int cc = min(c, JN - 1), t = cc % N;
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    const bool wx = ra.with_extra;
+    // every load of the workgroup at once, in the order they are waited on: the previous totals
+    // (the ranking), the extra rollout's cost rows (the stage; straight-line, so that no loop
+    // header waits on the loads after them), then the generated row and the candidates (needed
+    // only after the ranking and the t-chains), unconditional at clamped addresses
+    const double cl = ra.costs[min(lane, Kp - 1)];
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+    double sv[kPickStageLoads];
+    if (wx) {
+#pragma unroll
+        for (int u = 0; u < kPickStageLoads; ++u)
+            if (wbase + u * 256 < P) {
+                const int i = min(tid + u * 256, P - 1);
+                sv[u] = i < N ? ra.x_state[i] : ra.x_control[i - N];
+            }
+    }
+    const size_t og = (size_t)max(min(lane, Kg - 1), 0);
+    double nz = a.noise[og * JN + cc], st = a.state[og * N + t], ct = a.control[og * JN + cc];
+    const size_t oq = (size_t)min(lane, Kp);
+    const double qp = ra.spec_params[oq * JN + cc], qn = ra.spec_noise[oq * JN + cc], qc = ra.spec_ctl[oq * JN + cc];
+    const double* qrow = oq < (size_t)Kp ? ra.src_state + oq * N : ra.x_state;
+    const double qs = qrow[t];
+    STAMP(11);
+    if (wx) {
+#pragma unroll
+        for (int u = 0; u < kPickStageLoads; ++u)
+            if (tid + u * 256 < P) stage[tid + u * 256] = sv[u];
+        __syncthreads();
+    }
+    STAMP(12);
+    // the choice is the same for every column: wave 0 makes the extra rollout's total while wave 1
+    // ranks the K previous totals, and every wave reads both after one barrier
+    __shared__ int inv_s[64];   // the candidate of K-rank j
+    __shared__ double xt_s;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (wv == 0) {
+        if (wx) {
+            // Rollout::getCost's t-chain of the extra rollout's row l (lane l <= J), then the
+            // rows' sum in row order (candidate_total)
+            double x = 0.0;
+            if (lane <= J) {
+                const double* v = stage + (size_t)lane * N;
+                x = v[0];
+                int u0 = 1;
+                for (; u0 + 32 <= N; u0 += 32) {
+                    double b[32];
+#pragma unroll
+                    for (int u = 0; u < 32; ++u) b[u] = v[u0 + u];
+#pragma unroll
+                    for (int u = 0; u < 32; ++u) x += b[u];
+                }
+                for (; u0 < N; ++u0) x += v[u0];
+            }
+            double xt = readlane_f64(x, 0);
+            for (int d = 0; d < J; ++d) xt += readlane_f64(x, 1 + d);
+            if (xt != xt) xt = __builtin_inf();
+            if (lane == 0) xt_s = xt;
+        }
+    } else if (wv == 1) {
+        // lane l's K-rank: (total, index) ascending among the K previous rows (independent
+        // compares, eight at a time); lanes past K keep their own index, so that the push below
+        // is a permutation of the wave
+        int rank = 0;
+        for (int m0 = 0; m0 < Kp; m0 += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int m = min(m0 + u, Kp - 1);
+                const double cm = readlane_f64(cl, m);
+                rank += (int)(((cm < cl) | ((cm == cl) & (m < lane))) & (m0 + u < Kp));
+            }
+        }
+        if (lane >= Kp) rank = lane;
+        // lane rank(l) receives l: the inverse permutation
+        inv_s[lane] = __builtin_amdgcn_ds_permute(rank << 2, lane);
+    }
+    __syncthreads();
+    // reused row rr takes the candidate of K-rank rr, or the extra rollout, or K-rank rr - 1
+    // (reuse_choice's two compares)
+    const int rr = lane - Kg;
+    const int rrc = min(max(rr, 0), 63);
+    const int selA = inv_s[rrc], selB = rr > 0 ? inv_s[rrc - 1] : selA;
+    int src = min(selA, Kp);
+    STAMP(13);
+    if (wx) {
+        const double xt = xt_s;
+        const double cA = __shfl(cl, src, 64), cB = __shfl(cl, min(selB, Kp), 64);
+        if (!(cA < xt)) src = (rr > 0 && cB >= xt) ? min(selB, Kp) : Kp;
+    }
+    STAMP(14);
+    const double sp = __shfl(qp, src, 64), sn = __shfl(qn, src, 64), sc = __shfl(qc, src, 64),
+                 ss = __shfl(qs, src, 64);
+    if (!cok) return;
+    if (lane >= Kg) {
+        nz = sn;
+        st = ss;
+        ct = sc;
+        if (lane < K) {
+            const size_t o = (size_t)lane * JN + c;
+            params[o] = sp;
+            noise[o] = sn;
+            control[o] = sc;
+            if (c < N) ra.state[(size_t)lane * N + c] = ss;
+        }
+    }
+    STAMP(15);
+    wave_weights(a, c, lane, K, st + ct, nz);
+    STAMP(16);
+}
+
 STOMP_STAMP_ACCESSORS(weights)
+
+bool launch_weights_pick_ok(const WeightArgs& a, const ReuseArgs& ra)
+{
+    return a.mode == W_FUSED && !a.cum && a.K_loc == ra.K && ra.K < kSumBlock && ra.K_gen >= 0 &&
+           ra.K_gen + ra.Kr == ra.K && ra.spec_params && ra.spec_noise && ra.spec_ctl &&
+           (a.J + 1) * a.N <= kPickStageLoads * 256;
+}
+
+void launch_weights_pick(const WeightArgs& a, const ReuseArgs& ra, double* params, double* noise, double* control,
+                         hipStream_t s)
+{
+    const size_t lds = ra.with_extra ? (size_t)(a.J + 1) * a.N * sizeof(double) : 0;
+    hipLaunchKernelGGL(k_weights_wave_pick, dim3((a.J * a.N + 3) / 4), dim3(256), lds, s, a, ra, params, noise,
+                       control);
+}
 
 // columns per workgroup of the column-tile kernel (k_weights, the fallback past the row tiles): as
 // many as keep K_loc * TC <= 2048

@@ -358,6 +358,12 @@ bool launch_reuse_pick_ok(const NoiseArgs& a, int K, int Kr);
 // launch carries pricing blocks
 int rollout_split_pieces(const DevModel& m, int nro, int extra_blocks, bool spec);
 void launch_reuse_pick(const NoiseArgs& a, const ReuseArgs& ra, hipStream_t s);
+// launch_reuse_pick folded into the one-wave-per-column weights (K < 64, no cumulative costs):
+// the reused rows' params / noise / control (and ra.state) written column by column as the
+// weights read them.  Only when launch_weights_pick_ok.
+bool launch_weights_pick_ok(const WeightArgs& a, const ReuseArgs& ra);
+void launch_weights_pick(const WeightArgs& a, const ReuseArgs& ra, double* params, double* noise, double* control,
+                         hipStream_t s);
 size_t price_candidate_lds_bytes(int J, int N);
 // the theta-independent part of generateRollouts + computeProjectedNoise for rows [0, rows):
 // normals, eps = sigma L z and M eps into a.pre_eps / a.pre_meps (run ahead on a side stream)

@@ -220,15 +220,18 @@ def test_iterations_bitwise(K, Kr):
         _compare_iteration(o, e, it)
 
 
-@pytest.mark.parametrize("no_spec", ["0", "1"])
-@pytest.mark.parametrize("dof,K,Kr", [(7, 20, 10), (14, 16, 6), (7, 12, 11), (7, 96, 40), (7, 130, 129)])
-def test_reused_rows_priced_ahead_or_after_bitwise(monkeypatch, no_spec, dof, K, Kr):
+@pytest.mark.parametrize("mode", ["fused", "pick", "no_spec"])
+@pytest.mark.parametrize("dof,K,Kr", [(7, 20, 10), (14, 16, 6), (7, 12, 11), (7, 63, 30), (7, 96, 40), (7, 130, 129)])
+def test_reused_rows_priced_ahead_or_after_bitwise(monkeypatch, mode, dof, K, Kr):
     # the reuse step on one device: every candidate priced by the rollout launch and the chosen
-    # one copied (k_reuse_pick), or (STOMP_DEBUG_NO_SPEC=1) the chosen row priced after the
-    # ranking (k_noise_rows<REUSE>); K_r = K - 1 reaches the lowest-ranked candidates; K > 64
+    # one copied in the weights launch (K < 64: k_weights_wave_pick) or by its own launch
+    # (STOMP_DEBUG_NO_PICK_FUSE=1, and K >= 64: k_reuse_pick), or (STOMP_DEBUG_NO_SPEC=1) the
+    # chosen row priced after the ranking (k_noise_rows<REUSE>); K_r = K - 1 reaches the
+    # lowest-ranked candidates; K = 63 fills the wave with the extra rollout's lane; K > 64
     # takes reuse_choice's ranking through the shared sel[] array (k_noise.hip), at K = 96 in the
     # split launch with its pricing blocks, at K = 130 (131 rollouts: no split) in the slot loop
-    monkeypatch.setenv("STOMP_DEBUG_NO_SPEC", no_spec)
+    monkeypatch.setenv("STOMP_DEBUG_NO_SPEC", "1" if mode == "no_spec" else "0")
+    monkeypatch.setenv("STOMP_DEBUG_NO_PICK_FUSE", "1" if mode == "pick" else "0")
     p = make(dof=dof, K=K, Kr=Kr)
     o, e = po.Oracle(p, threads=8), eng.Engine(p)
     for it in range(1, 7):

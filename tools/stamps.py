@@ -88,7 +88,10 @@ if KR > 0:
     show("misc", 0, lambda i: {0: "k_reuse: start", 1: "rows staged", 2: "t-chains", 3: "total counted",
                                10: "last: start", 11: "last: totals loaded", 12: "last: ranked",
                                13: "last: rows copied"}.get(i, str(i)))
-show("weights", 0, lambda i: ["start", "min/max", "exp", "psum", "u partials", "end", "tile loaded"][i])
+WEIGHT_LABELS = {0: "start", 1: "min/max", 2: "exp", 3: "psum", 4: "u partials", 5: "end", 6: "tile loaded",
+                 10: "pick: start", 11: "pick: loads issued", 12: "pick: staged (barrier)", 13: "pick: ranked",
+                 14: "pick: extra total / choice", 15: "pick: rows written", 16: "pick: weights done"}
+show("weights", 0, lambda i: WEIGHT_LABELS.get(i, str(i)))
 
 
 def residency():
