@@ -1768,6 +1768,8 @@ int stomp_engine_create(const stomp_engine_desc* d, stomp_engine** out)
     {
         const char* env = std::getenv("STOMP_DEBUG_SPLIT_MAX");
         m.split_max = env ? std::atoi(env) : 0;
+        const char* xi = std::getenv("STOMP_DEBUG_XCTL_INLINE");
+        m.x_ctl_inline = xi && std::strcmp(xi, "1") == 0 ? 1 : 0;
     }
     m.pad_collision = 0;
     launch_pad_fk(m, e->d_start, e->d_goal, e->d_pad_pos, e->d_pad_cf, e->stream);

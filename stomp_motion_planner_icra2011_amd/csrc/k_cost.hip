@@ -346,6 +346,32 @@ __device__ __forceinline__ void spec_block(const CostArgs& a, int c, double* lds
                                   threadIdx.x);
 }
 
+// a split launch's last block (CostArgs::x_ctl_block): the extra rollout's rows of addExtraRollouts
+// (theta copied, noise 0, the control costs of theta + 0), which its first piece made ahead of its
+// row before; zA / zB: the block's LDS
+template <int BLOCK>
+__device__ __forceinline__ void x_ctl_rows_block(const CostArgs& a, int Nall, double* zA, double* zB)
+{
+    if (a.stop && *a.stop) return;
+    const int J = a.nz.J, N = a.nz.N, tid = threadIdx.x;
+    for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = a.x_params[min(idx0 + tid + u * BLOCK, J * N - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = idx0 + tid + u * BLOCK;
+            if (idx < J * N) {
+                a.x_prm[idx] = v[u];
+                a.x_nse[idx] = 0.0;
+                const int d = idx / N, i = idx - d * N;
+                zA[d * Nall + i + 6] = v[u] + 0.0;
+            }
+        }
+    }
+    rollout_control<BLOCK>(a.nz, 0, zA, zB, tid, a.x_ctl);
+}
+
 // the rollout kernel's workgroup `bid` of one engine's launch (k_rollout: bid = blockIdx.x;
 // k_rollout_group: the engines of a group share one launch)
 // FK_OVERLAP: the slot loop's FK lanes advance the program to the next sphere segment while the
@@ -1023,7 +1049,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
     double* zB = (double*)(lds_raw + L.zB);
     if (bid >= nro * P) {
         const int r = bid - nro * P;
-        if (r >= a.pre_rows + a.tot_rows) spec_block<BLOCK>(a, r - a.pre_rows - a.tot_rows, (double*)lds_raw);
+        if (r >= a.pre_rows + a.tot_rows + a.spec_rows) x_ctl_rows_block<BLOCK>(a, m.Nall, zA, zB);
+        else if (r >= a.pre_rows + a.tot_rows) spec_block<BLOCK>(a, r - a.pre_rows - a.tot_rows, (double*)lds_raw);
         else if (r >= a.pre_rows) totals_block<BLOCK>(a, J, N, r - a.pre_rows, zA);   // zA, zB: contiguous
         else pregen_block<BLOCK>(a, r, false, zA, zB);
         return;
@@ -1074,7 +1101,8 @@ __global__ __launch_bounds__(BLOCK, BLOCK > 256 ? 2 : 3) void k_rollout_split(De
         rollout_normals<BLOCK>(a.nz, e, zA, zB, tid);
     } else if (!pre) {
         const double* prm = extra ? a.x_params : a.params + (long long)e * a.stride;
-        const bool xc = extra && a.x_ctl && piece == 0;   // the extra rollout's rows (addExtraRollouts)
+        // the extra rollout's rows (addExtraRollouts), unless the launch's last block makes them
+        const bool xc = extra && a.x_ctl && piece == 0 && !a.x_ctl_block;
         for (int idx0 = 0; idx0 < J * N; idx0 += 4 * BLOCK) {
             double v[4];
 #pragma unroll
@@ -1496,9 +1524,11 @@ static void launch_cost_t(const DevModel& m, const CostArgs& a, hipStream_t s)
         CostArgs b = a;
         b.split = P;
         b.split_cnt = m.split_cnt;
+        // the extra rollout's control rows on a block of their own when one more fits the CUs
+        b.x_ctl_block = a.x_params && a.x_ctl && !m.x_ctl_inline && nro * P + extra_blocks + 1 <= m.cus ? 1 : 0;
         lds_opt_in((const void*)k_rollout_split<kSplitBlock, BRICK>, ls);
-        hipLaunchKernelGGL((k_rollout_split<kSplitBlock, BRICK>), dim3(nro * P + extra_blocks), dim3(kSplitBlock), ls,
-                           s, m, b);
+        hipLaunchKernelGGL((k_rollout_split<kSplitBlock, BRICK>), dim3(nro * P + extra_blocks + b.x_ctl_block),
+                           dim3(kSplitBlock), ls, s, m, b);
         return;
     }
     assert(a.spec_rows == 0);   // the engine asks rollout_split_pieces first

@@ -102,6 +102,8 @@ struct DevModel {
                                 // eval batches included); split_pieces refuses larger launches
     int split_cap;
     int split_max;              // most pieces per rollout (STOMP_DEBUG_SPLIT_MAX, read at creation)
+    int x_ctl_inline;           // STOMP_DEBUG_XCTL_INLINE=1: the extra rollout's control rows by its
+                                // first piece (CostArgs::x_ctl_block never set)
     // LDS-lean slot-loop layout (rollout_lds lean > 0), chosen at creation when it fits more rollout
     // workgroups on a CU than the full layout and the launch has more workgroups than the full
     // layout's slots (cfg3's N = 199, cfg4's two-arm tree): 1 = the saved branch-point frames in HBM
@@ -247,6 +249,10 @@ struct CostArgs {
     double* spec_params;        // [K + 1][J][N]
     double* spec_noise;
     double* spec_ctl;
+    // split launches: the extra rollout's theta copy, zero noise and control costs (x_ctl) made by
+    // one block after the pricing blocks instead of by the extra rollout's first piece ahead of its
+    // row (set by launch_cost when the launch splits and x_ctl is wanted)
+    int x_ctl_block;
 };
 
 enum WeightMode { W_FUSED = 0, W_MINMAX = 1, W_PSUM = 2, W_USUM = 3 };

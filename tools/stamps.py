@@ -80,6 +80,23 @@ def cost_label(i):
 show("cost", 1, cost_label)   # a noisy rollout of the last iteration launch (odd: FK on waves 2-3)
 show("cost", 2, cost_label)   # an even one (FK on waves 0-1, thread 0 stamps inside the FK lanes)
 show("cost", 0, cost_label)   # the last launch: the flushed noiseless rollout
+for b in [int(x) for x in os.environ.get("STAMP_COST_BLOCKS", "").split(",") if x]:
+    show("cost", b, cost_label)   # chosen blocks (a split launch: rollout e's piece p is e P + p)
+if os.environ.get("STAMP_SPAN"):
+    # start / end of every workgroup of the last launch that ran it (block records), relative
+    # to the earliest start: which pieces finish last
+    fn = lib.stomp_debug_blocks_cost
+    fn.argtypes = [C.c_void_p]
+    bb = np.zeros((8192, 6), np.uint64)
+    e.run(6, 1)
+    e.synchronize()
+    fn(bb.ctypes.data)
+    n = int(os.environ["STAMP_SPAN"])
+    rec = bb[:n].astype(np.int64)
+    lo = rec[:, 2][rec[:, 2] > 0].min()
+    for i in range(n):
+        if rec[i, 2] > 0:
+            print(f"    block {i:4d} start {int(rec[i, 2] - lo):8d} end {int(rec[i, 3] - lo):8d}")
 NOISE_LABELS = {0: "start", 6: "reuse: loads in, staged", 10: "reuse: K-ranked", 11: "reuse: row loads issued", 12: "reuse: t-chains (wave 0)", 7: "reuse: barrier", 1: "rows loaded / normals", 2: "M eps (rows) / L z", 3: "M eps", 4: "control", 5: "end",
                 9: "control: padding", 61: "control terms (thread 0)", 62: "control terms barrier",
                 63: "control costs stored (t0)"}
