@@ -56,15 +56,18 @@ __device__ __forceinline__ void update_tile(int J, int N, const double* MT, cons
     if (tid >= kUpdCols) return;
     double s = 0.0;
     int k = 0;
-    for (; k + 8 <= N; k += 8) {
-        double a[8], x[8];
+    // 32 terms' LDS reads in flight per wait (8 at a time: cfg2 16.27k -> 16.48k it/s,
+    // profiles/ab/r6_update_batch.txt)
+    constexpr int kB = 32;
+    for (; k + kB <= N; k += kB) {
+        double a[kB], x[kB];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < kB; ++q) {
             a[q] = ms[(k + q) * kUpdCols + tid];
             x[q] = us[k + q];
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s += a[q] * x[q];
+        for (int q = 0; q < kB; ++q) s += a[q] * x[q];
     }
     for (; k < N; ++k) s += ms[k * kUpdCols + tid] * us[k];
     if (tid >= nc || stopped) return;
